@@ -1,0 +1,371 @@
+// libmimo_engine: C-ABI host side of the MI355X Monte-Carlo BER engine.
+//
+// Coarse seam = mp_model.Link (mp_model.py:32-329).  mimo_engine_run launches the fused
+// trial kernel (trial_kernel.h) over a batch of trials, reduces the per-trial counts on
+// the device and adds the totals into the caller's counters, like Link.simulate adds
+// into its shared mp.Array counters (mp_model.py:217-222).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mimo_engine.h"
+#include "trial_launch.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess) return fail(MIMO_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+constexpr double kSpeedOfLight = 299792458.0;  // scipy.constants.c
+
+bool is_pow2(long v) { return v > 0 && (v & (v - 1)) == 0; }
+
+// Sum of per-trial counts over trials, per counter index (deterministic order-free
+// integer sums; one 64-bit atomic per wave).
+__global__ void reduce_counts(const uint32_t* __restrict__ c, uint64_t n_trials, int n_idx,
+                              unsigned long long* __restrict__ tot) {
+  const int idx = blockIdx.y;
+  unsigned long long acc = 0;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_trials; t += (uint64_t)gridDim.x * blockDim.x)
+    acc += c[t * n_idx + idx];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&tot[idx], acc);
+}
+
+}  // namespace
+
+namespace mimo {
+void set_error(const std::string& m) { g_err = m; }
+}  // namespace mimo
+
+struct mimo_engine {
+  mimo_config cfg{};
+  std::vector<double> tx_pos, freqs;
+  mimo_point pt{};
+  bool have_point = false;
+  // device state (created lazily on the first run: fork safety)
+  bool ready = false;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  float2* d_tw = nullptr;
+  float* d_ant_rel = nullptr;
+  float* d_f_rel = nullptr;
+  double* d_f_over_c = nullptr;
+  double* d_tx_pos = nullptr;
+  uint32_t* d_counts = nullptr;
+  size_t counts_cap = 0;
+  unsigned long long* d_tot = nullptr;
+  double d0 = 1.0;
+  double last_ms = 0.0;
+  std::string desc;
+};
+
+namespace {
+
+int team_for(int F) { return mimo::team_size(F); }
+
+mimo::InstanceKey select_instance(const mimo_engine* e, bool csi) {
+  mimo::InstanceKey k{};
+  k.F = e->cfg.n_fft;
+  k.T = team_for(k.F);
+  const int S = e->cfg.n_sub_carr;
+  const int P = k.F / k.T;
+  k.aligned = (S % (4 * k.T) == 0) && S < k.F && (S / k.T == 8 || S / k.T == 4) && (S / k.T) < P;
+  k.nslot = k.aligned ? S / k.T : P;
+  k.ch = e->cfg.channel_kind;
+  k.csi = csi;
+  return k;
+}
+
+hipError_t launch(const mimo::InstanceKey& k, dim3 grid, hipStream_t st, const mimo::TrialParams& p, bool* found) {
+  switch (k.F) {
+    case 128: return mimo::launch_trial_F128(k, grid, st, p, found);
+    case 256: return mimo::launch_trial_F256(k, grid, st, p, found);
+    case 512: return mimo::launch_trial_F512(k, grid, st, p, found);
+    case 1024: return mimo::launch_trial_F1024(k, grid, st, p, found);
+    case 2048: return mimo::launch_trial_F2048(k, grid, st, p, found);
+    case 4096: return mimo::launch_trial_F4096(k, grid, st, p, found);
+    case 8192: return mimo::launch_trial_F8192(k, grid, st, p, found);
+    default: *found = false; return hipSuccess;
+  }
+}
+
+int validate_config(const mimo_config* c) {
+  if (!c) return fail(MIMO_EINVAL, "null config");
+  if (!is_pow2(c->n_fft) || c->n_fft < 128 || c->n_fft > 8192)
+    return fail(MIMO_EINVAL, "n_fft must be a power of two in [128, 8192]");
+  if (c->n_sub_carr < 4 || c->n_sub_carr % 4 || c->n_sub_carr > c->n_fft - 2)
+    return fail(MIMO_EINVAL, "n_sub_carr must be a multiple of 4 in [4, n_fft - 2] (modulation.py:266-267 overlap)");
+  const int L = (int)std::lround(std::sqrt((double)c->constel_size));
+  if (L * L != c->constel_size || !is_pow2(c->constel_size) || c->constel_size < 4 || c->constel_size > 4096)
+    return fail(MIMO_EINVAL, "Constellation size must be a power of some number, only square QAM supported.");
+  if (c->n_ant < 1 || c->n_ant > 4096) return fail(MIMO_EINVAL, "n_ant must be in [1, 4096]");
+  if (c->channel_kind < MIMO_CH_RAYLEIGH || c->channel_kind > MIMO_CH_TWOPATH)
+    return fail(MIMO_EINVAL, "unknown channel_kind");
+  if (c->receiver_kind != MIMO_RX_CNC && c->receiver_kind != MIMO_RX_MCNC)
+    return fail(MIMO_EINVAL, "unknown receiver_kind");
+  if (!c->tx_pos) return fail(MIMO_EINVAL, "tx_pos is required");
+  return MIMO_OK;
+}
+
+int ensure_device(mimo_engine* e) {
+  if (e->ready) return MIMO_OK;
+  if (e->cfg.device >= 0) HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipGetDevice(&e->device));
+  HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreate(&e->ev0));
+  HIP_TRY(hipEventCreate(&e->ev1));
+  const int F = e->cfg.n_fft, S = e->cfg.n_sub_carr, A = e->cfg.n_ant;
+  // twiddles exp(-j 2 pi e / F), computed in double
+  std::vector<float2> tw(F);
+  for (int i = 0; i < F; ++i) {
+    const double ang = -2.0 * M_PI * (double)i / (double)F;
+    tw[i] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+  }
+  // in-band sub-carrier k -> bin (modulation.py:266-267)
+  std::vector<float> f_rel(S);
+  std::vector<double> f_over_c(S);
+  const double fc = e->freqs[0];  // bin 0 = centre frequency
+  for (int k = 0; k < S; ++k) {
+    const int bin = k < S / 2 ? F - S / 2 + k : k - S / 2 + 1;
+    const double f = e->freqs[bin];
+    f_rel[k] = (float)(fc / f);
+    f_over_c[k] = f / kSpeedOfLight;
+  }
+  // Rayleigh FSPL at the nominal RX (channel.py:216-225), relative to the nearest antenna
+  std::vector<double> dist(A);
+  double dmin = 1e300;
+  for (int a = 0; a < A; ++a) {
+    const double dx = e->tx_pos[3 * a] - e->cfg.rx_pos[0], dy = e->tx_pos[3 * a + 1] - e->cfg.rx_pos[1],
+                 dz = e->tx_pos[3 * a + 2] - e->cfg.rx_pos[2];
+    dist[a] = std::sqrt(dx * dx + dy * dy + dz * dz);
+    dmin = std::min(dmin, dist[a]);
+  }
+  e->d0 = dmin > 0 ? dmin : 1.0;
+  std::vector<float> ant_rel(A);
+  for (int a = 0; a < A; ++a) ant_rel[a] = (float)(e->d0 / dist[a]);
+
+  HIP_TRY(hipMalloc(&e->d_tw, sizeof(float2) * F));
+  HIP_TRY(hipMalloc(&e->d_f_rel, sizeof(float) * S));
+  HIP_TRY(hipMalloc(&e->d_f_over_c, sizeof(double) * S));
+  HIP_TRY(hipMalloc(&e->d_ant_rel, sizeof(float) * A));
+  HIP_TRY(hipMalloc(&e->d_tx_pos, sizeof(double) * 3 * A));
+  HIP_TRY(hipMalloc(&e->d_tot, sizeof(unsigned long long) * 64));
+  HIP_TRY(hipMemcpy(e->d_tw, tw.data(), sizeof(float2) * F, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_f_rel, f_rel.data(), sizeof(float) * S, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_f_over_c, f_over_c.data(), sizeof(double) * S, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_ant_rel, ant_rel.data(), sizeof(float) * A, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_tx_pos, e->tx_pos.data(), sizeof(double) * 3 * A, hipMemcpyHostToDevice));
+  e->ready = true;
+  return MIMO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t mimo_abi_version(void) { return MIMO_ABI_VERSION; }
+const char* mimo_last_error(void) { return g_err.c_str(); }
+
+int32_t mimo_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+mimo_engine* mimo_engine_create(const mimo_config* cfg) {
+  if (validate_config(cfg) != MIMO_OK) return nullptr;
+  auto* e = new mimo_engine();
+  e->cfg = *cfg;
+  const int A = cfg->n_ant, F = cfg->n_fft;
+  e->tx_pos.assign(cfg->tx_pos, cfg->tx_pos + 3 * A);
+  e->freqs.resize(F);
+  if (cfg->carrier_freqs) {
+    std::copy(cfg->carrier_freqs, cfg->carrier_freqs + F, e->freqs.begin());
+  } else {
+    fail(MIMO_EINVAL, "carrier_freqs is required");
+    delete e;
+    return nullptr;
+  }
+  e->cfg.tx_pos = nullptr;
+  e->cfg.carrier_freqs = nullptr;
+  return e;
+}
+
+int32_t mimo_engine_set_point(mimo_engine* e, const mimo_point* pt) {
+  if (!e || !pt) return fail(MIMO_EINVAL, "null argument");
+  auto bad_kind = [](int k) { return k < MIMO_PA_NONE || k > MIMO_PA_TOI; };
+  if (bad_kind(pt->pa_kind) || bad_kind(pt->cnc_pa_kind)) return fail(MIMO_EINVAL, "unknown PA kind");
+  if ((pt->pa_kind == MIMO_PA_SOFTLIM || pt->pa_kind == MIMO_PA_RAPP) && !(pt->sat_pow > 0))
+    return fail(MIMO_EINVAL, "sat_pow must be > 0");
+  if (pt->pa_kind == MIMO_PA_RAPP && !(pt->p_hardness > 0)) return fail(MIMO_EINVAL, "p_hardness must be > 0");
+  if (!(pt->cnc_alpha != 0)) return fail(MIMO_EINVAL, "cnc_alpha must be non-zero");
+  if (pt->csi_eps >= 1.0) return fail(MIMO_EINVAL, "csi_eps must be < 1");
+  if (pt->csi_eps >= 0 && e->cfg.n_ant > 1024) return fail(MIMO_EINVAL, "CSI error supports n_ant <= 1024");
+  e->pt = *pt;
+  e->have_point = true;
+  return MIMO_OK;
+}
+
+int32_t mimo_engine_run(mimo_engine* e, uint64_t seed, uint64_t first_trial, uint64_t n_trials, const int32_t* iters,
+                        int32_t n_iters, int32_t incl_clean, uint64_t* err_out, uint64_t* bits_out, uint32_t* per_trial) {
+  if (!e) return fail(MIMO_EINVAL, "null engine");
+  if (!e->have_point) return fail(MIMO_EINVAL, "mimo_engine_set_point was not called");
+  if (n_iters < 1 || !iters) return fail(MIMO_EINVAL, "at least one iteration index is required");
+  uint32_t rec_mask = 0;
+  int max_iter = -1;
+  for (int i = 0; i < n_iters; ++i) {
+    if (iters[i] < 0 || iters[i] > 31) return fail(MIMO_EINVAL, "iterations must be in [0, 31]");
+    if (i && iters[i] <= iters[i - 1]) return fail(MIMO_EINVAL, "iterations must be sorted and unique");
+    rec_mask |= 1u << iters[i];
+    max_iter = std::max(max_iter, (int)iters[i]);
+  }
+  if (!err_out || !bits_out) return fail(MIMO_EINVAL, "null counters");
+  const int n_idx = n_iters + (incl_clean ? 1 : 0);
+  const mimo_config& c = e->cfg;
+  const mimo_point& pt = e->pt;
+  if (n_trials + first_trial > (1ull << 32)) return fail(MIMO_EINVAL, "trial index must fit 32 bits");
+  const bool csi = pt.csi_eps >= 0;
+  const mimo::InstanceKey key = select_instance(e, csi);
+  if (int rc = ensure_device(e)) return rc;
+
+  mimo::TrialParams p{};
+  p.seed = seed;
+  p.tw = e->d_tw;
+  p.ant_rel = e->d_ant_rel;
+  p.f_rel = e->d_f_rel;
+  p.f_over_c = e->d_f_over_c;
+  p.tx_pos = e->d_tx_pos;
+  p.n_ant = c.n_ant;
+  p.n_sc = c.n_sub_carr;
+  const int L = (int)std::lround(std::sqrt((double)c.constel_size));
+  p.qam_l = L;
+  p.half_bits = (int)std::lround(std::log2((double)L));
+  p.label_mask = (uint32_t)c.constel_size - 1u;
+  p.pa_kind = pt.pa_kind;
+  p.cnc_pa_kind = pt.cnc_pa_kind;
+  p.sat_tx = (float)pt.sat_pow;
+  p.sqrt_sat_tx = (float)std::sqrt(std::max(pt.sat_pow, 0.0));
+  p.inv_sat_tx = pt.sat_pow > 0 ? (float)(1.0 / pt.sat_pow) : 0.f;
+  p.rapp_p = (float)pt.p_hardness;
+  p.toi_tx = (float)pt.toi_coeff;
+  p.sat_cnc = (float)pt.cnc_sat_pow;
+  p.sqrt_sat_cnc = (float)std::sqrt(std::max(pt.cnc_sat_pow, 0.0));
+  p.inv_sat_cnc = pt.cnc_sat_pow > 0 ? (float)(1.0 / pt.cnc_sat_pow) : 0.f;
+  p.toi_cnc = (float)pt.cnc_toi_coeff;
+  p.inv_alpha_cnc = (float)(1.0 / pt.cnc_alpha);
+  p.alpha_c = (float)(std::pow(10.0, pt.ibo_db / 10.0) * c.n_sub_carr / c.n_ant);
+  p.es_over_snr = (float)(pt.avg_symbol_power / std::pow(10.0, pt.snr_db / 10.0));
+  p.csi_a = csi ? (float)std::sqrt(1.0 - pt.csi_eps * pt.csi_eps) : 1.f;
+  p.csi_b = csi ? (float)pt.csi_eps : 0.f;
+  p.inv_sqrt_f = (float)(1.0 / std::sqrt((double)c.n_fft));
+  p.receiver = c.receiver_kind;
+  p.max_iter = max_iter;
+  p.rec_mask = rec_mask;
+  p.incl_clean = incl_clean ? 1 : 0;
+  p.n_idx = n_idx;
+  p.rx_x0 = c.rx_pos[0];
+  p.rx_z = c.rx_pos[2];
+  p.rx_var = c.reroll_chan ? c.rx_loc_var : 0.0;
+  p.d0 = e->d0;
+  if (!c.reroll_chan && c.channel_kind != MIMO_CH_RAYLEIGH) {
+    // fixed RX: jitter span 0 around (x0, x0); only consistent when rx_y == rx_x
+    if (c.rx_pos[1] != c.rx_pos[0]) return fail(MIMO_EINVAL, "reroll_chan=0 requires rx_pos[1] == rx_pos[0]");
+  }
+
+  char buf[160];
+  snprintf(buf, sizeof buf, "F=%d T=%d slots=%d %s ch=%d csi=%d", key.F, key.T, key.nslot,
+           key.aligned ? "aligned" : "generic", key.ch, (int)key.csi);
+  e->desc = buf;
+
+  const uint64_t chunk_max = 1ull << 20;
+  const size_t need = (size_t)std::min<uint64_t>(n_trials, chunk_max) * n_idx;
+  if (need > e->counts_cap) {
+    if (e->d_counts) HIP_TRY(hipFree(e->d_counts));
+    HIP_TRY(hipMalloc(&e->d_counts, need * sizeof(uint32_t)));
+    e->counts_cap = need;
+  }
+  HIP_TRY(hipMemsetAsync(e->d_tot, 0, sizeof(unsigned long long) * n_idx, e->stream));
+  double ms_total = 0.0;
+  for (uint64_t done = 0; done < n_trials; done += chunk_max) {
+    const uint64_t nt = std::min<uint64_t>(chunk_max, n_trials - done);
+    p.first_trial = first_trial + done;
+    p.counts = e->d_counts;
+    HIP_TRY(hipEventRecord(e->ev0, e->stream));
+    bool found = false;
+    hipError_t le = launch(key, dim3((unsigned)nt), e->stream, p, &found);
+    if (!found) return fail(MIMO_ENOKERNEL, std::string("no kernel instance for ") + buf);
+    if (le != hipSuccess) return fail(MIMO_EHIP, std::string("trial kernel launch: ") + hipGetErrorString(le));
+    HIP_TRY(hipEventRecord(e->ev1, e->stream));
+    hipLaunchKernelGGL(reduce_counts, dim3(64, n_idx), dim3(256), 0, e->stream, e->d_counts, nt, n_idx, e->d_tot);
+    HIP_TRY(hipGetLastError());
+    if (per_trial)
+      HIP_TRY(hipMemcpyAsync(per_trial + done * n_idx, e->d_counts, nt * n_idx * sizeof(uint32_t),
+                             hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipEventSynchronize(e->ev1));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+    ms_total += ms;
+  }
+  unsigned long long tot[64];
+  HIP_TRY(hipMemcpyAsync(tot, e->d_tot, sizeof(unsigned long long) * n_idx, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  const uint64_t bits_per_trial = (uint64_t)c.n_sub_carr * (uint64_t)std::lround(std::log2((double)c.constel_size));
+  for (int i = 0; i < n_idx; ++i) {
+    err_out[i] += tot[i];
+    bits_out[i] += bits_per_trial * n_trials;
+  }
+  e->last_ms = ms_total;
+  return MIMO_OK;
+}
+
+double mimo_engine_last_kernel_ms(const mimo_engine* e) { return e ? e->last_ms : 0.0; }
+
+const char* mimo_engine_describe(const mimo_engine* e) {
+  if (!e) return "";
+  if (e->desc.empty()) {
+    const mimo::InstanceKey k = select_instance(e, e->have_point && e->pt.csi_eps >= 0);
+    char buf[160];
+    snprintf(buf, sizeof buf, "F=%d T=%d slots=%d %s ch=%d csi=%d", k.F, k.T, k.nslot,
+             k.aligned ? "aligned" : "generic", k.ch, (int)k.csi);
+    const_cast<mimo_engine*>(e)->desc = buf;
+  }
+  return e->desc.c_str();
+}
+
+void mimo_engine_destroy(mimo_engine* e) {
+  if (!e) return;
+  if (e->ready) {
+    (void)hipStreamSynchronize(e->stream);
+    (void)hipFree(e->d_tw);
+    (void)hipFree(e->d_f_rel);
+    (void)hipFree(e->d_f_over_c);
+    (void)hipFree(e->d_ant_rel);
+    (void)hipFree(e->d_tx_pos);
+    (void)hipFree(e->d_tot);
+    if (e->d_counts) (void)hipFree(e->d_counts);
+    (void)hipEventDestroy(e->ev0);
+    (void)hipEventDestroy(e->ev1);
+    (void)hipStreamDestroy(e->stream);
+  }
+  delete e;
+}
+
+}  // extern "C"

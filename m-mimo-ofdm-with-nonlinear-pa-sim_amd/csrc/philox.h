@@ -1,0 +1,77 @@
+// Device-side Philox4x32-10 and the engine's random-stream layout (gfx950).
+//
+// One statement of the layout lives in oracle/philox.py (the CPU checker); this is the
+// device statement, and tests/test_gpu_*.py pin the two against each other.
+//   key = (seed_lo32, seed_hi32);  counter = (element, trial, stream, aux)
+//   BITS  (k>>2, trial, 1, 0)  -> word[k&3] & (M-1) = QAM label of sub-carrier k
+//   CHAN  (q,    trial, 2, a)  -> 2 CN(0,1) draws, sub-carrier pair q, antenna a
+//   NOISE (q,    trial, 3, 0)  -> 2 CN(0,1) draws
+//   CSI   (q,    trial, 4, a)  -> 2 CN(0,1) draws
+//   LOC   (0,    trial, 5, 0)  -> 2 uniforms (RX position jitter)
+// Replaces the reference's sequential PCG64 streams (mp_model.py:121-125,
+// channel.py:209-212) with counter-addressed ones so that every trial is reproducible
+// on any device count and in any order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mimo {
+
+enum Stream : uint32_t { ST_BITS = 1, ST_CHAN = 2, ST_NOISE = 3, ST_CSI = 4, ST_LOC = 5 };
+
+struct Key {
+  uint32_t k0, k1;
+};
+
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, Key key) {
+  uint32_t k0 = key.k0, k1 = key.k1;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint32_t lo0 = 0xD2511F53u * c.x;
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+  }
+  return c;
+}
+
+// Box-Muller on two words -> CN(0,1):  sqrt(-ln u1) * exp(j 2 pi u2),
+// u1 = (w0 + 0.5) 2^-32, u2 = w1 2^-32.  v_sin/v_cos take revolutions, so 2*pi*u2 is
+// never formed; v_log is log2.
+__device__ __forceinline__ float2 box_muller(uint32_t w0, uint32_t w1) {
+  const float u1 = fmaf((float)w0, 2.3283064365386963e-10f, 1.1641532182693481e-10f);
+  const float u2 = (float)w1 * 2.3283064365386963e-10f;
+  const float rho = __builtin_sqrtf(-0.69314718055994531f * __builtin_amdgcn_logf(u1));
+  const float rev = u2 >= 1.0f ? 0.0f : u2;  // (float)w1 may round up to 2^32
+  return make_float2(rho * __builtin_amdgcn_cosf(rev), rho * __builtin_amdgcn_sinf(rev));
+}
+
+__device__ __forceinline__ void cn_pair(Key key, uint32_t q, uint32_t trial, uint32_t stream, uint32_t aux,
+                                        float2& z1, float2& z2) {
+  const uint4 w = philox4x32_10(make_uint4(q, trial, stream, aux), key);
+  z1 = box_muller(w.x, w.y);
+  z2 = box_muller(w.z, w.w);
+}
+
+// Quarter pairing: sub-carrier k -> pair index q and slot (0: k1, 1: k2 = k1 + S/4).
+__device__ __forceinline__ void pair_of(int k, int n_sc, uint32_t& q, int& slot) {
+  const int half = n_sc >> 1, quarter = n_sc >> 2;
+  const int h = k >= half ? 1 : 0;
+  const int r = k - h * half;
+  slot = r >= quarter ? 1 : 0;
+  q = (uint32_t)(h * quarter + r - slot * quarter);
+}
+
+__device__ __forceinline__ uint32_t qam_label(Key key, int k, uint32_t trial, uint32_t mask) {
+  const uint4 w = philox4x32_10(make_uint4((uint32_t)k >> 2, trial, ST_BITS, 0u), key);
+  const int s = k & 3;
+  const uint32_t word = s == 0 ? w.x : s == 1 ? w.y : s == 2 ? w.z : w.w;
+  return word & mask;
+}
+
+}  // namespace mimo

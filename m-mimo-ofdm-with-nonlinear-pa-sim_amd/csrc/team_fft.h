@@ -1,0 +1,206 @@
+// Workgroup ("team") FFT for the fused trial kernel — gfx950, fp32.
+//
+// Replaces the reference's per-antenna torch CPU FFTs (modulation.py:270,
+// utilities.py:329, corrector.py:93,98): ortho IFFT/FFT of one F-point OFDM symbol.
+//
+// Layout: the team has T threads (T = 64 * waves); thread t holds P = F/T complex
+// points in registers in the CYCLIC distribution, element e at (thread e % T,
+// register e / T).  A Stockham autosort radix-R stage reads, for butterfly
+// j = t + T*i, the elements j + r*F/R = t + T*(i + r*P/R): all in the thread's own
+// registers.  The last stage writes j + r*F/R as well, so input and output are both
+// cyclic and a transform needs (stages - 1) exchanges through a padded LDS buffer
+// (one pad slot per 32 elements: conflict-free ds_write_b64 / ds_read_b64 for the
+// stage patterns used here).  F = 2048 with P = 16 is radix 16 x 16 x 8: two
+// exchanges, four barriers.
+//
+// Scaling is left to the caller (transforms are un-normalised).  DIR = -1 forward
+// (e^{-j2pi nk/F}), +1 inverse.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mimo {
+
+// ---------------------------------------------------------------- compile-time trig
+constexpr double kPi = 3.14159265358979323846264338327950288;
+
+constexpr double ct_cos(double x) {
+  while (x > kPi) x -= 2 * kPi;
+  while (x < -kPi) x += 2 * kPi;
+  double term = 1.0, sum = 1.0;
+  for (int n = 1; n < 40; ++n) {
+    term *= -x * x / ((2.0 * n - 1.0) * (2.0 * n));
+    sum += term;
+  }
+  return sum;
+}
+constexpr double ct_sin(double x) { return ct_cos(x - kPi / 2); }
+
+constexpr int ilog2(int n) { return n <= 1 ? 0 : 1 + ilog2(n >> 1); }
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {  // a * conj(b)
+  return make_float2(fmaf(a.x, b.x, a.y * b.y), fmaf(a.y, b.x, -a.x * b.y));
+}
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+
+// x * exp(DIR * j * 2 pi * M / R) with the trivial angles resolved at compile time.
+template <int M, int R, int DIR>
+__device__ __forceinline__ float2 ctw(float2 x) {
+  constexpr int m = ((M % R) + R) % R;
+  if constexpr (m == 0) {
+    return x;
+  } else if constexpr (4 * m == R) {  // DIR * j
+    return DIR > 0 ? make_float2(-x.y, x.x) : make_float2(x.y, -x.x);
+  } else if constexpr (2 * m == R) {
+    return make_float2(-x.x, -x.y);
+  } else if constexpr (4 * m == 3 * R) {  // -DIR * j
+    return DIR > 0 ? make_float2(x.y, -x.x) : make_float2(-x.y, x.x);
+  } else {
+    constexpr float c = (float)ct_cos(2.0 * kPi * m / R);
+    constexpr float s = (float)(DIR * ct_sin(2.0 * kPi * m / R));
+    return make_float2(fmaf(x.x, c, -x.y * s), fmaf(x.x, s, x.y * c));
+  }
+}
+
+// In-register DFT of size R (natural order in and out), four-step R = R1 x R2.
+template <int R, int DIR>
+struct Dft {
+  static __device__ __forceinline__ void run(float2* v) {
+    if constexpr (R == 1) {
+      return;
+    } else if constexpr (R == 2) {
+      const float2 a = v[0], b = v[1];
+      v[0] = cadd(a, b);
+      v[1] = csub(a, b);
+    } else if constexpr (R == 4) {
+      const float2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+      const float2 t2 = cadd(v[1], v[3]), t3 = ctw<1, 4, DIR>(csub(v[1], v[3]));
+      v[0] = cadd(t0, t2);
+      v[2] = csub(t0, t2);
+      v[1] = cadd(t1, t3);
+      v[3] = csub(t1, t3);
+    } else {
+      constexpr int R1 = (R >= 16) ? 4 : 2;
+      constexpr int R2 = R / R1;
+      float2 sub[R1][R2];
+#pragma unroll
+      for (int n1 = 0; n1 < R1; ++n1) {
+#pragma unroll
+        for (int n2 = 0; n2 < R2; ++n2) sub[n1][n2] = v[n1 + R1 * n2];
+        Dft<R2, DIR>::run(sub[n1]);
+      }
+      Twid<R1, R2, 1, 0>::apply(sub);
+#pragma unroll
+      for (int k2 = 0; k2 < R2; ++k2) {
+        float2 col[R1];
+#pragma unroll
+        for (int n1 = 0; n1 < R1; ++n1) col[n1] = sub[n1][k2];
+        Dft<R1, DIR>::run(col);
+#pragma unroll
+        for (int k1 = 0; k1 < R1; ++k1) v[k2 + R2 * k1] = col[k1];
+      }
+    }
+  }
+
+  // sub[n1][k2] *= W_R^(n1 k2), unrolled with compile-time indices.
+  template <int R1, int R2, int N1, int K2>
+  struct Twid {
+    template <typename A>
+    static __device__ __forceinline__ void apply(A& sub) {
+      if constexpr (N1 < R1) {
+        if constexpr (K2 < R2) {
+          sub[N1][K2] = ctw<N1 * K2, R, DIR>(sub[N1][K2]);
+          Twid<R1, R2, N1, K2 + 1>::apply(sub);
+        } else {
+          Twid<R1, R2, N1 + 1, 0>::apply(sub);
+        }
+      }
+    }
+  };
+};
+
+// ---------------------------------------------------------------- team FFT
+template <int F, int T>
+struct TeamFft {
+  static constexpr int P = F / T;
+  static constexpr int LOG_F = ilog2(F);
+  static constexpr int LOG_P = ilog2(P);
+  static constexpr int NST = (LOG_F + LOG_P - 1) / LOG_P;
+  static constexpr int LDS_ELEMS = F + F / 32;
+  static_assert((1 << LOG_F) == F && (1 << LOG_P) == P && P >= 2, "power-of-two sizes");
+
+  static constexpr int bits(int s) { return LOG_F / NST + (s < LOG_F % NST ? 1 : 0); }
+  static constexpr int bits_before(int s) { return s == 0 ? 0 : bits_before(s - 1) + bits(s - 1); }
+  static __device__ __forceinline__ int pad(int e) { return e + (e >> 5); }
+
+  template <int S, int DIR>
+  static __device__ __forceinline__ void stage(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t) {
+    constexpr int R = 1 << bits(S);
+    constexpr int NS = 1 << bits_before(S);
+    constexpr int B = P / R;
+    constexpr bool LAST = (S == NST - 1);
+    static_assert(B >= 1 && B * R == P, "radix must divide points per thread");
+    if constexpr (!LAST) __syncthreads();  // every thread has read the previous exchange
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      float2 v[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = d[i + r * B];
+      const int j = t + T * i;
+      const int jm = j & (NS - 1);
+      if constexpr (NS > 1) {
+        const int step = jm * (F / (NS * R));
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+          const float2 w = tw[step * r];  // exp(-j 2 pi e / F)
+          v[r] = DIR < 0 ? cmul(v[r], w) : cmulc(v[r], w);
+        }
+      }
+      Dft<R, DIR>::run(v);
+      if constexpr (LAST) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) d[i + r * B] = v[r];
+      } else {
+        const int base = (j / NS) * NS * R + jm;
+#pragma unroll
+        for (int r = 0; r < R; ++r) lds[pad(base + r * NS)] = v[r];
+      }
+    }
+    if constexpr (!LAST) {
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < P; ++m) d[m] = lds[pad(t + T * m)];
+    }
+  }
+
+  template <int S, int DIR>
+  static __device__ __forceinline__ void stages(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t) {
+    if constexpr (S < NST) {
+      stage<S, DIR>(d, lds, tw, t);
+      stages<S + 1, DIR>(d, lds, tw, t);
+    }
+  }
+
+  // Un-normalised transform of the team's cyclic-distributed vector.  Ends with the
+  // last exchange's reads done by this thread only: callers that touch `lds` next must
+  // barrier first (the next transform's first exchange does).
+  //
+  // The twiddles and LDS addresses depend only on the thread id, so inside the
+  // caller's antenna loop LICM would hoist all of them (~60 VGPRs) out of the loop and
+  // spill.  Laundering t and tw through empty asm makes them opaque per transform:
+  // they are re-derived (cheap ALU + L1-hit loads) instead of held.
+  template <int DIR>
+  static __device__ __forceinline__ void run(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t) {
+    const float2* twl = tw;
+    int tl = t;
+    asm volatile("" : "+s"(twl));
+    asm volatile("" : "+v"(tl));
+    stages<0, DIR>(d, lds, twl, tl);
+  }
+};
+
+}  // namespace mimo

@@ -1,0 +1,548 @@
+// Fused Monte-Carlo BER trial kernel for gfx950 (MI355X).
+//
+// One workgroup ("team", T threads) runs one trial = one OFDM symbol of
+// mp_model.Link.simulate (mp_model.py:180-222; clean run :133-175) entirely on chip:
+//
+//   labels (Philox BITS)                                  mp_model.py:208
+//   pass 1: channel draws -> MRT norms sum_a |H|^2         antenna_array.py:162-173
+//   pass 3: per antenna a
+//       H (Philox CHAN x FSPL, or closed-form LoS/two-path)  channel.py:35-72,116-167,262-275
+//       alpha_a from the per-antenna precoding power      mp_model.py:312-326
+//       X = s conj(H) / ||H||  -> IFFT -> PA -> FFT       modulation.py:332-361, distortion.py, utilities.py:311-329
+//       r += H Y,  g += alpha_a |H|^2 / ||H||             channel.py:287-290, mp_model.py:320-326
+//   AWGN (Philox NOISE) scaled by Es eta / snr, z = (r + n)/g   noise.py:56-83, mp_model.py:210-214
+//   CNC (corrector.py:52-112) or MCNC (corrector.py:165-207) iterations, hard slicer,
+//   XOR-popcount bit errors -> counts[trial][idx]         mp_model.py:215-222
+//
+// Nothing per trial touches HBM except the final per-trial counts (n_idx x 4 B): the
+// channel is regenerated from Philox instead of being stored.
+// Frequency-domain data live in the team FFT's cyclic register layout; each thread
+// owns NSLOT in-band sub-carriers ("slots").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "philox.h"
+#include "team_fft.h"
+
+namespace mimo {
+
+enum PaKind : int { PA_NONE = 0, PA_SOFTLIM = 1, PA_RAPP = 2, PA_TOI = 3 };
+enum ChanKind : int { CH_RAYLEIGH = 1, CH_LOS = 2, CH_TWOPATH = 3 };
+enum RxKind : int { RX_CNC = 1, RX_MCNC = 2 };
+
+constexpr int kMaxWaves = 16;
+
+struct TrialParams {
+  uint64_t seed;
+  uint64_t first_trial;
+  uint32_t* counts;              // [n_trials][n_idx]
+  const float2* tw;              // [F] exp(-j 2 pi e / F)
+  const float* ant_rel;          // [A]  d0 / d_a      (Rayleigh FSPL, relative)
+  const float* f_rel;            // [S]  fc / f_k      (f_k float32-quantised as in the reference)
+  const double* f_over_c;        // [S]  f_k / c       (LoS / two-path phases)
+  const double* tx_pos;          // [A*3]
+  int n_ant, n_sc, qam_l, half_bits;
+  uint32_t label_mask;
+  int pa_kind, cnc_pa_kind;
+  float sat_tx, sqrt_sat_tx, inv_sat_tx, rapp_p, toi_tx;
+  float sat_cnc, sqrt_sat_cnc, inv_sat_cnc, toi_cnc, inv_alpha_cnc;
+  float alpha_c;                 // 10^(IBO/10) S / A : gamma_a^2 = alpha_c / vk_pow[a]
+  float es_over_snr;             // Es / 10^(SNR/10)
+  float csi_a, csi_b;            // sqrt(1 - eps^2), eps
+  float inv_sqrt_f;
+  int receiver;
+  int max_iter;                  // largest iteration index to run (CNC / MCNC)
+  uint32_t rec_mask;             // bit i: record iteration i
+  int incl_clean, n_idx;
+  double rx_x0, rx_z, rx_var, d0; // LoS / two-path geometry
+};
+
+// ---------------------------------------------------------------- slot geometry
+// ALIGNED: S % (4T) == 0 and S < F.  Slot s < HALF is the positive band (bin
+// n = t + T s, k = n + S/2 - 1; thread 0 slot 0 is bin S/2 instead of DC); slot s >= HALF
+// is the negative band (bin F - S/2 + t + T (s - HALF), k = t + T (s - HALF)).
+// Generic: slot s = register s, valid iff its bin is in band.
+template <int F, int T, int NSLOT, bool ALIGNED>
+struct Slots {
+  static constexpr int P = F / T;
+  static constexpr int HALF = NSLOT / 2;
+  static constexpr int m_of(int s) { return ALIGNED ? (s < HALF ? s : P - NSLOT + s) : s; }
+
+  static __device__ __forceinline__ int k_of(int s, int t, int S, bool& valid) {
+    if constexpr (ALIGNED) {
+      valid = true;
+      if (s < HALF) {
+        const int n = (s == 0 && t == 0) ? (S >> 1) : t + T * s;
+        return n + (S >> 1) - 1;
+      }
+      return t + T * (s - HALF);
+    } else {
+      const int n = t + T * s;
+      const int lo = F - (S >> 1);
+      valid = (n >= 1 && n <= (S >> 1)) || n >= lo;
+      return !valid ? 0 : (n >= lo ? n - lo : n + (S >> 1) - 1);  // 0 keeps table reads in bounds
+    }
+  }
+
+  static __device__ __forceinline__ void scatter(float2 (&d)[P], const float2 (&x)[NSLOT], bool t0) {
+#pragma unroll
+    for (int m = 0; m < P; ++m) d[m] = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int s = 0; s < NSLOT; ++s) {
+      if constexpr (ALIGNED) {
+        if (s == 0) {
+          d[0] = t0 ? make_float2(0.f, 0.f) : x[0];
+          d[HALF] = t0 ? x[0] : make_float2(0.f, 0.f);
+          continue;
+        }
+      }
+      d[m_of(s)] = x[s];
+    }
+  }
+
+  static __device__ __forceinline__ float2 gather(const float2 (&d)[P], int s, bool t0) {
+    if constexpr (ALIGNED) {
+      if (s == 0) return t0 ? d[HALF] : d[0];
+    }
+    return d[m_of(s)];
+  }
+};
+
+// ---------------------------------------------------------------- small helpers
+// Opaque copy: stops LICM from hoisting thread-invariant derived values (slot->k maps,
+// Philox round-0 products, QAM points, table loads) out of the antenna loop, which
+// would keep dozens of VGPRs live across it and spill.  Re-deriving them is cheap.
+template <typename V>
+__device__ __forceinline__ V opaque(V v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Team-wide sum; every thread gets the result.  Two barriers.
+template <int T>
+__device__ __forceinline__ float team_sum(float v, float* red) {
+  v = wave_sum(v);
+  if constexpr (T == 64) {
+    return v;
+  } else {
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < T / 64; ++i) s += red[i];
+    return s;
+  }
+}
+
+// Bussgang gain, modulation.py:178-189, from gamma^2.
+__device__ __forceinline__ float alpha_of_gamma2(float g2) {
+  const float g = __builtin_sqrtf(g2);
+  return 1.0f - __expf(-g2) + 0.88622692545275801f * g * erfcf(g);
+}
+
+// PA on one time-domain sample (distortion.py:9-19, 102-113, 202-211).
+__device__ __forceinline__ float2 pa_apply(int kind, float2 x, float sat, float sqrt_sat, float inv_sat, float rapp_p,
+                                           float toi) {
+  const float pw = fmaf(x.x, x.x, x.y * x.y);
+  float sc = 1.0f;
+  if (kind == PA_SOFTLIM) {
+    sc = pw > sat ? sqrt_sat * __builtin_amdgcn_rsqf(pw) : 1.0f;
+  } else if (kind == PA_RAPP) {
+    // 1 / (1 + (pw/sat)^p)^(1/(2p))
+    const float u = pw * inv_sat;
+    const float up = u > 0.f ? __builtin_amdgcn_exp2f(rapp_p * __builtin_amdgcn_logf(u)) : 0.f;
+    sc = __builtin_amdgcn_exp2f(-(0.5f / rapp_p) * __builtin_amdgcn_logf(1.0f + up));
+  } else if (kind == PA_TOI) {
+    sc = 1.0f - toi * pw;
+  }
+  return make_float2(x.x * sc, x.y * sc);
+}
+
+// Per-axis hard slicer == argmin |z - C| over the Gray-ordered constellation with the
+// reference's first-index (lowest label) tie-break (modulation.py:75-76,138-146).
+__device__ __forceinline__ uint32_t gray(uint32_t i) { return i ^ (i >> 1); }
+__device__ __forceinline__ uint32_t gray_inv(uint32_t g) {
+  g ^= g >> 1;
+  g ^= g >> 2;
+  g ^= g >> 4;
+  g ^= g >> 8;
+  return g;
+}
+__device__ __forceinline__ uint32_t slice_axis(float x, int L) {
+  const float q = (x + (float)L) * 0.5f;
+  float fi = floorf(q);
+  int i = (int)fi;
+  if (q == fi && i > 0 && i < L) {  // exact midpoint between levels i-1 and i
+    i = gray((uint32_t)(i - 1)) < gray((uint32_t)i) ? i - 1 : i;
+  }
+  i = i < 0 ? 0 : (i > L - 1 ? L - 1 : i);
+  return gray((uint32_t)i);
+}
+__device__ __forceinline__ uint32_t slice(float2 z, int L, int hb) {
+  return (slice_axis(z.x, L) << hb) | slice_axis(z.y, L);
+}
+__device__ __forceinline__ float2 qam_point(uint32_t label, int L, int hb) {
+  const uint32_t ii = gray_inv(label >> hb), iq = gray_inv(label & ((1u << hb) - 1u));
+  return make_float2((float)(2 * (int)ii - (L - 1)), (float)(2 * (int)iq - (L - 1)));
+}
+
+// ---------------------------------------------------------------- channel generation
+template <int F, int T, int NSLOT, bool ALIGNED, int CH>
+struct Channel {
+  using SL = Slots<F, T, NSLOT, ALIGNED>;
+
+  // CN(0,1) draws of one stream for the thread's slots (pairs resolved in-thread when aligned).
+  static __device__ __forceinline__ void normals(Key key, uint32_t trial, uint32_t stream, uint32_t aux, int t, int S,
+                                                 float2 (&z)[NSLOT]) {
+    if constexpr (ALIGNED) {
+      constexpr int Q = SL::HALF / 2;
+#pragma unroll
+      for (int band = 0; band < 2; ++band) {
+#pragma unroll
+        for (int j = 0; j < Q; ++j) {
+          const int sa = band * SL::HALF + j, sb = sa + Q;
+          bool v;
+          const int k = SL::k_of(sa, t, S, v);
+          uint32_t q;
+          int slot;
+          pair_of(k, S, q, slot);
+          float2 z1, z2;
+          cn_pair(key, q, trial, stream, aux, z1, z2);
+          z[sa] = slot == 0 ? z1 : z2;
+          z[sb] = slot == 0 ? z2 : z1;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) {
+        bool v;
+        const int k = SL::k_of(s, t, S, v);
+        z[s] = make_float2(0.f, 0.f);
+        if (v) {
+          uint32_t q;
+          int slot;
+          pair_of(k, S, q, slot);
+          float2 z1, z2;
+          cn_pair(key, q, trial, stream, aux, z1, z2);
+          z[s] = slot == 0 ? z1 : z2;
+        }
+      }
+    }
+  }
+
+  // True channel of antenna a at the thread's slots (relative scale: common factors
+  // cancel in MRT, AGC and the SNR normalisation).
+  static __device__ __forceinline__ void gen(const TrialParams& p, Key key, uint32_t trial, int a, int t,
+                                             const double (&rx)[3], float2 (&h)[NSLOT]) {
+    const int S = p.n_sc;
+    if constexpr (CH == CH_RAYLEIGH) {
+      normals(key, trial, ST_CHAN, (uint32_t)a, t, S, h);
+      const float sa = p.ant_rel[a];
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) {
+        bool v;
+        const int k = SL::k_of(s, t, S, v);
+        const float sc = v ? sa * p.f_rel[k] : 0.f;
+        h[s] = cscale(h[s], sc);
+      }
+    } else {
+      const double tx = p.tx_pos[3 * a], ty = p.tx_pos[3 * a + 1], tz = p.tx_pos[3 * a + 2];
+      const double dx = tx - rx[0], dy = ty - rx[1], dz = tz - rx[2];
+      const double d_los = sqrt(dx * dx + dy * dy + dz * dz);
+      const float att_los = (float)(p.d0 / d_los);
+      double d_sec = 0.0;
+      float att_sec = 0.f;
+      if constexpr (CH == CH_TWOPATH) {
+        // channel.py:138-147: elevation from the mirrored geometry
+        const double horiz = sqrt(dx * dx + dy * dy);
+        const double elev = atan((tz + rx[2]) / horiz);
+        const double se = sin(elev);
+        d_sec = tz / se + rx[2] / se;
+        att_sec = (float)(p.d0 / d_sec);
+      }
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) {
+        bool v;
+        const int k = SL::k_of(s, t, S, v);
+        float2 hv = make_float2(0.f, 0.f);
+        if (v) {
+          const double foc = p.f_over_c[k];
+          const float fr = p.f_rel[k];
+          double ph = d_los * foc;
+          ph -= floor(ph);
+          const float a1 = att_los * fr;
+          hv = make_float2(a1 * __builtin_amdgcn_cosf((float)ph), a1 * __builtin_amdgcn_sinf((float)ph));
+          if constexpr (CH == CH_TWOPATH) {
+            double ph2 = d_sec * foc;
+            ph2 -= floor(ph2);
+            const float a2 = att_sec * fr;
+            hv.x -= a2 * __builtin_amdgcn_cosf((float)ph2);
+            hv.y -= a2 * __builtin_amdgcn_sinf((float)ph2);
+          }
+        }
+        h[s] = hv;
+      }
+    }
+  }
+};
+
+// ---------------------------------------------------------------- the kernel
+template <int F, int T, int NSLOT, bool ALIGNED, int CH, bool CSI, int MINW>
+__global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
+  using FFT = TeamFft<F, T>;
+  using SL = Slots<F, T, NSLOT, ALIGNED>;
+  using CHN = Channel<F, T, NSLOT, ALIGNED, CH>;
+  constexpr int P = FFT::P;
+  constexpr int W = T / 64;
+
+  __shared__ float2 lds[FFT::LDS_ELEMS];
+  __shared__ float red[kMaxWaves];
+  __shared__ float vk_part[2][kMaxWaves];
+  __shared__ float pw_csi[CSI ? 1024 : 1];
+
+  const int t = threadIdx.x;
+  const bool t0 = (t == 0);
+  const int lane = t & 63, wid = t >> 6;
+  const uint32_t trial = (uint32_t)(p.first_trial + blockIdx.x);
+  const Key key{(uint32_t)p.seed, (uint32_t)(p.seed >> 32)};
+  const int S = p.n_sc, A = p.n_ant, L = p.qam_l, hb = p.half_bits;
+  const float inv_sqrt_f = p.inv_sqrt_f;
+
+  // RX position for LoS / two-path (mp_model.py:190-201; y uses rx_loc_x, a reference quirk)
+  double rx[3] = {0.0, 0.0, 0.0};
+  if constexpr (CH != CH_RAYLEIGH) {
+    const uint4 w = philox4x32_10(make_uint4(0u, trial, ST_LOC, 0u), key);
+    const double u0 = (double)w.x * 2.3283064365386963e-10, u1 = (double)w.y * 2.3283064365386963e-10;
+    rx[0] = p.rx_x0 - p.rx_var * 0.5 + p.rx_var * u0;
+    rx[1] = p.rx_x0 - p.rx_var * 0.5 + p.rx_var * u1;
+    rx[2] = p.rx_z;
+  }
+
+  // ---- transmitted labels and validity
+  uint32_t lab[NSLOT];
+  uint32_t valid_mask = 0;
+#pragma unroll
+  for (int s = 0; s < NSLOT; ++s) {
+    bool v;
+    const int k = SL::k_of(s, t, S, v);
+    lab[s] = v ? qam_label(key, k, trial, p.label_mask) : 0u;
+    valid_mask |= (v ? 1u : 0u) << s;
+  }
+
+  // ---- pass 1: MRT norms over the (estimated) channel
+  float nrm2[NSLOT];
+#pragma unroll
+  for (int s = 0; s < NSLOT; ++s) nrm2[s] = 0.f;
+  for (int a = 0; a < A; ++a) {
+    const int tl = opaque(t);
+    float2 h[NSLOT];
+    CHN::gen(p, key, trial, a, tl, rx, h);
+    if constexpr (CSI) {
+      // mp_model.py:264-282: Hhat = sqrt(1-eps^2) H + eps sqrt(mean_k |H|^2) z
+      float pw = 0.f;
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) pw = fmaf(h[s].x, h[s].x, fmaf(h[s].y, h[s].y, pw));
+      pw = team_sum<T>(pw, red) / (float)S;
+      if (t0) pw_csi[a] = pw;
+      float2 zc[NSLOT];
+      CHN::normals(key, trial, ST_CSI, (uint32_t)a, tl, S, zc);
+      const float sc = p.csi_b * __builtin_sqrtf(pw);
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s)
+        h[s] = make_float2(fmaf(p.csi_a, h[s].x, sc * zc[s].x), fmaf(p.csi_a, h[s].y, sc * zc[s].y));
+    }
+#pragma unroll
+    for (int s = 0; s < NSLOT; ++s) nrm2[s] = fmaf(h[s].x, h[s].x, fmaf(h[s].y, h[s].y, nrm2[s]));
+  }
+  float inv_nrm[NSLOT];
+  float etac_p = 0.f;  // sum_k ||Hhat_k||^2 for the clean-run noise scaler (mp_model.py:304)
+#pragma unroll
+  for (int s = 0; s < NSLOT; ++s) {
+    const bool v = (valid_mask >> s) & 1u;
+    inv_nrm[s] = v ? __builtin_amdgcn_rsqf(nrm2[s]) : 0.f;
+    etac_p += v ? nrm2[s] : 0.f;
+  }
+  if constexpr (CSI) __syncthreads();  // pw_csi visible
+
+  float2 d[P];
+  float2 r[NSLOT];
+  float g[NSLOT];
+  float2 cc[CSI ? NSLOT : 1];  // clean-run combine sum_a H conj(Hhat)/||Hhat|| (CSI only)
+#pragma unroll
+  for (int s = 0; s < NSLOT; ++s) {
+    r[s] = make_float2(0.f, 0.f);
+    g[s] = 0.f;
+    if constexpr (CSI) cc[s] = make_float2(0.f, 0.f);
+  }
+
+  // ---- array pass: precode -> IFFT -> PA -> FFT -> combine, one antenna at a time.
+  // MAIN: symbols = tx labels, combine with the true channel, accumulate g (alpha_a).
+  // MCNC: symbols = detected labels, combine with the estimated channel (corrector.py:198-200).
+  auto array_pass = [&](const uint32_t (&sym_lab)[NSLOT], bool main_pass, float2 (&acc)[NSLOT])
+                        __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < NSLOT; ++s) acc[s] = make_float2(0.f, 0.f);
+    for (int a = 0; a < A; ++a) {
+      const int tl = opaque(t);
+      uint32_t sl[NSLOT];
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) sl[s] = opaque(sym_lab[s]);
+      float2 h[NSLOT];
+      CHN::gen(p, key, trial, a, tl, rx, h);
+      float2 he[CSI ? NSLOT : 1];
+      if constexpr (CSI) {
+        float2 zc[NSLOT];
+        CHN::normals(key, trial, ST_CSI, (uint32_t)a, tl, S, zc);
+        const float sc = p.csi_b * __builtin_sqrtf(pw_csi[a]);
+#pragma unroll
+        for (int s = 0; s < NSLOT; ++s)
+          he[s] = make_float2(fmaf(p.csi_a, h[s].x, sc * zc[s].x), fmaf(p.csi_a, h[s].y, sc * zc[s].y));
+      }
+      auto hest = [&](int s) __attribute__((always_inline)) -> float2 {
+        if constexpr (CSI) return he[s]; else return h[s];
+      };
+      float2 x[NSLOT];
+      float vk = 0.f;
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) {
+        const float2 e = hest(s);
+        const float wgt = inv_nrm[s] * inv_sqrt_f;
+        const float2 sym = qam_point(sl[s], L, hb);
+        x[s] = cscale(cmulc(sym, e), wgt);  // s conj(Hhat) / ||Hhat|| / sqrt(F)
+        if ((valid_mask >> s) & 1u) {
+          const float e2 = fmaf(e.x, e.x, e.y * e.y);
+          vk = fmaf(e2, inv_nrm[s] * inv_nrm[s], vk);
+        } else {
+          x[s] = make_float2(0.f, 0.f);
+        }
+      }
+      if (main_pass) {
+        vk = wave_sum(vk);
+        if (lane == 0) vk_part[a & 1][wid] = vk;  // read after the IFFT's first barrier
+      }
+      SL::scatter(d, x, t0);
+      FFT::template run<+1>(d, lds, p.tw, t);
+#pragma unroll
+      for (int m = 0; m < P; ++m)
+        d[m] = pa_apply(p.pa_kind, d[m], p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
+      FFT::template run<-1>(d, lds, p.tw, t);
+      float alpha_a = 0.f;
+      if (main_pass) {
+        float vks = 0.f;
+#pragma unroll
+        for (int i = 0; i < W; ++i) vks += vk_part[a & 1][i];
+        alpha_a = alpha_of_gamma2(p.alpha_c / vks);
+      }
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) {
+        const float2 y = SL::gather(d, s, t0);
+        if (main_pass) {
+          acc[s] = cadd(acc[s], cmul(h[s], y));
+          const float2 e = hest(s);
+          g[s] = fmaf(alpha_a * inv_nrm[s], fmaf(e.x, e.x, e.y * e.y), g[s]);
+          if constexpr (CSI) cc[s] = cadd(cc[s], cscale(cmulc(h[s], e), inv_nrm[s]));
+        } else {
+          acc[s] = cadd(acc[s], cmul(hest(s), y));
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < NSLOT; ++s) acc[s] = cscale(acc[s], inv_sqrt_f);
+  };
+
+  array_pass(lab, true, r);
+
+  // ---- AWGN + AGC (noise.py:56-83 on all bins; only in-band bins matter)
+  float2 zn[NSLOT];
+  CHN::normals(key, trial, ST_NOISE, 0u, t, S, zn);
+  float eta_p = 0.f;
+#pragma unroll
+  for (int s = 0; s < NSLOT; ++s) eta_p = ((valid_mask >> s) & 1u) ? fmaf(g[s], g[s], eta_p) : eta_p;
+  const float eta = team_sum<T>(eta_p, red) / (float)S;
+  uint32_t* out = p.counts + (size_t)blockIdx.x * p.n_idx;
+
+  auto record = [&](int idx, uint32_t errs) __attribute__((always_inline)) {
+    const float tot = team_sum<T>((float)errs, red);
+    if (t0) out[idx] = (uint32_t)(tot + 0.5f);
+  };
+
+  if (p.incl_clean) {
+    // clean run (mp_model.py:159-175): no PA, AGC / noise from sum_a Hhat P = ||Hhat||
+    const float etac = team_sum<T>(etac_p, red) / (float)S;
+    const float sig_c = __builtin_sqrtf(p.es_over_snr * etac);
+    uint32_t errs = 0;
+#pragma unroll
+    for (int s = 0; s < NSLOT; ++s) {
+      const float2 sym = qam_point(lab[s], L, hb);
+      float2 rc;
+      if constexpr (CSI) rc = cmul(cc[s], sym); else rc = cscale(sym, inv_nrm[s] > 0.f ? 1.0f / inv_nrm[s] : 0.f);
+      const float ig = inv_nrm[s];  // 1 / ||Hhat||
+      const float2 zc = make_float2((rc.x + sig_c * zn[s].x) * ig, (rc.y + sig_c * zn[s].y) * ig);
+      const uint32_t lh = slice(zc, L, hb);
+      errs += ((valid_mask >> s) & 1u) ? __popc(lh ^ lab[s]) : 0u;
+    }
+    record(0, errs);
+  }
+
+  const float sig = __builtin_sqrtf(p.es_over_snr * eta);
+  float2 z[NSLOT];
+#pragma unroll
+  for (int s = 0; s < NSLOT; ++s) {
+    const float ig = ((valid_mask >> s) & 1u) ? 1.0f / g[s] : 0.f;
+    z[s] = make_float2((r[s].x + sig * zn[s].x) * ig, (r[s].y + sig * zn[s].y) * ig);
+  }
+
+  // ---- CNC / MCNC receiver
+  float2 dist[NSLOT];
+#pragma unroll
+  for (int s = 0; s < NSLOT; ++s) dist[s] = make_float2(0.f, 0.f);
+  int idx = p.incl_clean;
+  for (int it = 0; it <= p.max_iter; ++it) {
+    uint32_t lh[NSLOT];
+    uint32_t errs = 0;
+#pragma unroll
+    for (int s = 0; s < NSLOT; ++s) {
+      lh[s] = slice(csub(z[s], dist[s]), L, hb);
+      errs += ((valid_mask >> s) & 1u) ? __popc(lh[s] ^ lab[s]) : 0u;
+    }
+    if ((p.rec_mask >> it) & 1u) record(idx++, errs);
+    if (it == p.max_iter) break;
+    if (p.receiver == RX_CNC) {
+      // corrector.py:84-110: single-antenna re-synthesis of the clipping distortion
+      float2 x[NSLOT];
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s)
+        x[s] = ((valid_mask >> s) & 1u) ? cscale(qam_point(lh[s], L, hb), inv_sqrt_f) : make_float2(0.f, 0.f);
+      SL::scatter(d, x, t0);
+      FFT::template run<+1>(d, lds, p.tw, t);
+#pragma unroll
+      for (int m = 0; m < P; ++m)
+        d[m] = pa_apply(p.cnc_pa_kind, d[m], p.sat_cnc, p.sqrt_sat_cnc, p.inv_sat_cnc, p.rapp_p, p.toi_cnc);
+      FFT::template run<-1>(d, lds, p.tw, t);
+      const float sc = inv_sqrt_f * p.inv_alpha_cnc;
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) {
+        const float2 y = SL::gather(d, s, t0);
+        dist[s] = ((valid_mask >> s) & 1u) ? csub(cscale(y, sc), qam_point(lh[s], L, hb)) : make_float2(0.f, 0.f);
+      }
+    } else {
+      float2 est[NSLOT];
+      array_pass(lh, false, est);
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) {
+        const float ig = ((valid_mask >> s) & 1u) ? 1.0f / g[s] : 0.f;
+        dist[s] = ((valid_mask >> s) & 1u) ? csub(cscale(est[s], ig), qam_point(lh[s], L, hb))
+                                           : make_float2(0.f, 0.f);
+      }
+    }
+  }
+}
+
+}  // namespace mimo

@@ -1,0 +1,29 @@
+"""Test-side helpers: build a GPU Engine for an oracle SimConfig (same system, same point)."""
+import numpy as np
+
+from oracle import refmath as rm
+from oracle.sim import SimConfig, point_params
+
+
+def engine_for(cfg: SimConfig, device=-1):
+    import _engine
+    carriers = rm.fftfreq_carriers(cfg.n_fft, cfg.carrier_spacing, cfg.center_freq)
+    eng = _engine.Engine(cfg.n_ant, cfg.n_sc, cfg.n_fft, cfg.constel_size, 4, cfg.channel, cfg.receiver, cfg.tx_pos,
+                         cfg.rx_pos, cfg.rx_loc_var, carriers, reroll=cfg.reroll, device=device)
+    pp = point_params(cfg)
+    avg = pp["avg_samp"] / cfg.n_ant  # MRT: mean |P|^2 = 1/A (antenna_array.py:328-335)
+    if cfg.pa == "toi":
+        kw = dict(toi_coeff=rm.toi_coeff(cfg.ibo_db, avg))
+    else:
+        kw = dict(sat_pow=rm.sat_pow(cfg.ibo_db, avg))
+    eng.set_point(cfg.ibo_db, cfg.snr_db, pp["es"], cfg.pa, p_hardness=cfg.p_hardness, cnc_pa_kind=cfg.pa,
+                  cnc_sat_pow=pp["cnc_sat"], cnc_toi_coeff=pp["cnc_coeff"], cnc_alpha=pp["cnc_alpha"],
+                  csi_eps=cfg.csi_eps, **kw)
+    return eng
+
+
+def count_agreement(a, b):
+    """Fraction of (trial, index) entries that agree exactly."""
+    a = np.asarray(a, np.int64)
+    b = np.asarray(b, np.int64)
+    return float(np.mean(a == b))
