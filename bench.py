@@ -1,0 +1,200 @@
+"""Headline benchmark: OFDM symbols/s/GPU of the Monte-Carlo BER chain (BASELINE config 2).
+
+Workload (BASELINE.json configs[1]): 64-antenna MRT, 1024 sub-carriers (FFT 2048), 64-QAM,
+soft-limiter PA at IBO 3 dB, i.i.d. Rayleigh channel rerolled per trial, Eb/N0 15 dB,
+standard receiver (iteration 0), 2^16 trials (= OFDM symbols) per step.  One step = one
+fused-kernel launch over the batch + the on-device count reduction.  Inputs are generated
+on the device from Philox streams (no host transfer).  ``--gpus N`` (torchrun, one rank
+per GPU) shards trials by index: weak scaling, no data-path collective; the per-step
+error counts are summed across ranks once at the end (RCCL all_reduce).
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "m-mimo-ofdm-with-nonlinear-pa-sim_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+A, S, F, M, CP = 64, 1024, 2048, 64, 128
+IBO, EBN0 = 3.0, 15.0
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3   # gfx950 dense FP32 (MFMA f32 == VALU f32 peak)
+
+
+def bytes_alg_per_trial(a=A, s=S, f=F):
+    """staged K1-K4 model, complex64 = 8 B:  8 A (6 S + 2 F)."""
+    return 8 * a * (6 * s + 2 * f)
+
+
+def flops_alg_per_trial(a=A, s=S, f=F):
+    """A (2 * 5 F log2 F + 14 S + 12 F)  (FFT pair + precode/PA/combine)."""
+    return a * (10 * f * np.log2(f) + 14 * s + 12 * f)
+
+
+def make_engine(device):
+    import _engine
+    import mp_model  # noqa: F401  (host mirror; computes the per-point scalars like Link)
+    from utilities import ebn0_to_snr
+    from modulation import OfdmQamModem
+    from antenna_array import LinearArray
+    from transceiver import Transceiver
+    from distortion import SoftLimiter
+    import channel, noise, copy
+
+    mod = OfdmQamModem(constel_size=M, n_fft=F, n_sub_carr=S, cp_len=CP)
+    dist = SoftLimiter(0, mod.avg_sample_power)
+    tx = Transceiver(modem=copy.deepcopy(mod), impairment=copy.deepcopy(dist), center_freq=int(3.5e9),
+                     carrier_spacing=int(15e3))
+    rx = Transceiver(modem=copy.deepcopy(mod), impairment=copy.deepcopy(dist), cord_x=212, cord_y=212, cord_z=1.5,
+                     center_freq=int(3.5e9), carrier_spacing=int(15e3))
+    arr = LinearArray(n_elements=A, base_transceiver=tx, center_freq=int(3.5e9), wav_len_spacing=0.5, cord_x=0,
+                      cord_y=0, cord_z=15)
+    ch = channel.MisoRayleighFd(tx_transceivers=arr.array_elements, rx_transceiver=rx, seed=1234)
+    link = mp_model.Link(mod_obj=mod, array_obj=arr, std_rx_obj=rx, chan_obj=ch, noise_obj=noise.Awgn(snr_db=10),
+                         rx_loc_var=10.0, n_err_min=10 ** 12, bits_sent_max=10 ** 15, is_mcnc=False, device=device)
+    link.update_distortion(ibo_val_db=IBO)
+    link.set_snr(ebn0_to_snr(EBN0, S, S, M))
+    return link.engine()
+
+
+def cpu_baseline(seconds=15.0):
+    """The float64 oracle (oracle/sim.py, NumPy, one process / one core) on a bounded sample
+    of the same workload: reported beside the GPU number, never the measured product."""
+    from oracle import refmath as rm
+    from oracle.sim import SimConfig, run_trials
+    cfg = SimConfig(A, S, F, M, pa="softlim", ibo_db=IBO, snr_db=float(rm.ebn0_to_snr(EBN0, S, S, M)))
+    run_trials(cfg, 7, [0], iters=[0])  # warm caches / imports
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        run_trials(cfg, 7, np.arange(n, n + 16), iters=[0])
+        n += 16
+    dt = time.perf_counter() - t0
+    return dict(value=round(n / dt, 3), unit="OFDM symbols/s", cores=1, kind="port",
+                sample=f"{n} trials of the config-2 chain (standard RX) through oracle/sim.py "
+                       f"(NumPy float64, 1 process, {dt:.1f} s)")
+
+
+def load_pmc_traffic(trials_per_launch):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if one matches."""
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("trials_per_launch") == trials_per_launch and "hbm_bytes_per_launch" in d:
+            return d["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1 << 16, help="trials (OFDM symbols) per GPU per step")
+    ap.add_argument("--iters", type=str, default="0", help="receiver iterations, e.g. 0 or 0,1,2,3,4")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    eng = make_engine(local)
+    iters = [int(x) for x in args.iters.split(",")]
+    B = args.batch
+    seed = 2137
+    err_tot = None
+
+    def step(i):
+        first = (i * world + rank) * B
+        e, b, _ = eng.run(seed, first, B, iters, False)
+        return e, b
+
+    for i in range(args.warmup):
+        step(i)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kern_ms = 0.0
+    for i in range(args.warmup, args.warmup + args.steps):
+        e, b = step(i)
+        kern_ms += eng.kernel_ms
+        err_tot = e if err_tot is None else err_tot + e
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        c = torch.tensor(err_tot.astype(np.int64), device=f"cuda:{local}")
+        dist.all_reduce(c)
+        err_tot = c.cpu().numpy()
+    total_trials = B * args.steps * world
+    value = total_trials / dt
+    avg_kernel_s = kern_ms / 1e3 / args.steps
+    b_alg = bytes_alg_per_trial() * B
+    f_alg = flops_alg_per_trial() * B
+    traffic, traffic_src = load_pmc_traffic(B)
+    out = {
+        "metric": "OFDM symbols/s/GPU (64-ant,1024-sc) + achieved HBM %peak; BER match vs ref",
+        "value": round(value, 1),
+        "unit": "OFDM symbols/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (on-device Philox bits / Rayleigh channel / AWGN)",
+        "config": {"workload": "BASELINE config 2: 64-ant MRT, 1024-sc (FFT 2048) 64-QAM, soft limiter IBO 3 dB, "
+                               "Rayleigh, Eb/N0 15 dB, standard RX",
+                   "trials_per_gpu_per_step": B, "iters": iters, "parallelism": f"trial-sharded x{world}"},
+        "roofline": {
+            "bound": "mfma", "regime": "fp32 VALU (gfx950 f32 MFMA peak == f32 VALU peak)",
+            "achieved": round(f_alg / avg_kernel_s / 1e12, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(f_alg / avg_kernel_s / 1e12 / FP32_PEAK_TFLOPS, 4),
+            "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": "mimo::trial_kernel<2048,128,8,aligned,rayleigh>", "kernel_ms": round(avg_kernel_s * 1e3, 3),
+            "flops_alg_per_trial": flops_alg_per_trial(),
+        },
+        "hbm_alg": {"achieved": round(b_alg / avg_kernel_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(b_alg / avg_kernel_s / 1e9 / HBM_PEAK_GBS, 4),
+                    "bytes_alg_per_trial": bytes_alg_per_trial(),
+                    "note": "SURVEY §8(d) staged-pipeline bytes; the fused kernel keeps them on chip"},
+        "ber": [round(float(x) / (total_trials * S * 6), 8) for x in err_tot],
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if dist:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,251 @@
+"""``Link`` -- the coarse drop-in seam (reference mp_model.py:16-329), MI355X build.
+
+Same constructor, methods and counter semantics as the reference, so the
+``main_mp_*`` drivers run unchanged with this directory first on ``sys.path``:
+``Link.simulate`` hands batches of trials to the fused HIP kernel
+(``libmimo_engine.so``: channel reroll, MRT, PA, FFTs, AWGN, AGC, CNC/MCNC, bit-error
+count all on the GPU) and adds the per-index totals into the caller's shared
+``mp.Array`` counters under their lock, with the reference's stopping rule
+(mp_model.py:137-138, 177-187).
+
+Differences, by design:
+* randomness: Philox streams keyed by ``seed_arr`` and addressed by trial index
+  instead of PCG64 generators; every forked process therefore gets independent
+  channels (the reference replays one Rayleigh sequence in all processes, channel.py:209-212);
+* a clean-run trial reuses its distorted trial's draws (no PA: the IFFT->FFT round
+  trip is the identity in-band), so both counters see the same channels and noise;
+* batches overshoot ``bits_sent_max`` by at most one batch, sized so they do not
+  (the reference overshoots by up to num_cores symbols).
+"""
+from __future__ import annotations
+
+import copy
+import multiprocessing
+
+import numpy as np
+from numpy import ndarray
+
+import _engine
+import channel
+import corrector
+import distortion
+from antenna_array import AntennaArray, sc_columns
+from modulation import OfdmQamModem
+from transceiver import Transceiver
+
+MAX_BATCH = 1 << 16
+
+
+def _seed64(seed_arr) -> int:
+    ss = np.random.SeedSequence([int(s) & 0xFFFFFFFFFFFFFFFF for s in np.atleast_1d(seed_arr)])
+    w = ss.generate_state(2, np.uint32)
+    return int(w[0]) | (int(w[1]) << 32)
+
+
+def _default_device():
+    """Device for this process: mp child k -> GPU k % n (drivers fork one Link per core)."""
+    ident = getattr(multiprocessing.current_process(), "_identity", ())
+    n = _engine.lib().mimo_device_count()
+    if n < 1:
+        raise _engine.EngineError("no HIP device visible")
+    return (ident[0] - 1) % n if ident else 0
+
+
+class Link:
+    """(mp_model.py:16-87)"""
+
+    def __init__(self, mod_obj: OfdmQamModem, array_obj: AntennaArray, std_rx_obj: Transceiver, chan_obj, noise_obj,
+                 rx_loc_var: float, n_err_min: int, bits_sent_max: int, is_mcnc: bool = False,
+                 csi_epsylon: float = None, device: int = None, max_batch: int = MAX_BATCH):
+        self.my_mod = copy.deepcopy(mod_obj)
+        self.my_array = copy.deepcopy(array_obj)
+        self.my_standard_rx = copy.deepcopy(std_rx_obj)
+        self.rx_loc_x = self.my_standard_rx.cord_x
+        self.rx_loc_y = self.my_standard_rx.cord_y
+        self.my_noise = copy.deepcopy(noise_obj)
+        self.my_csi_noise = copy.deepcopy(noise_obj)
+        self.csi_epsylon = csi_epsylon
+        if not isinstance(chan_obj, (channel.MisoRayleighFd, channel.MisoLosFd, channel.MisoTwoPathFd)):
+            raise NotImplementedError(f"{type(chan_obj).__name__} is out of scope (MATLAB / NumPy-1 channels)")
+        self.is_quadriga = False
+        self.my_miso_chan = copy.deepcopy(chan_obj)
+        if self.csi_epsylon is not None:
+            self.my_miso_chan_csi_err = copy.deepcopy(self.my_miso_chan)
+        self.is_mcnc = is_mcnc
+        if is_mcnc:
+            self.my_cnc_rx = corrector.McncReceiver(self.my_array, self.my_miso_chan, _host_setup=True)
+        else:
+            self.my_cnc_rx = corrector.CncReceiver(copy.deepcopy(array_obj.base_transceiver.modem),
+                                                   copy.deepcopy(array_obj.base_transceiver.impairment))
+        self.my_noise.rng_gen = np.random.default_rng(0)
+        self.loc_rng = np.random.default_rng(1)
+        self.bit_rng = np.random.default_rng(2)
+        self.my_csi_noise.rng_gen = np.random.default_rng(3)
+        self.rx_loc_var = rx_loc_var
+        self.n_ant_val = len(self.my_array.array_elements)
+        self.n_bits_per_ofdm_sym = self.my_mod.n_bits_per_ofdm_sym
+        self.n_sub_carr = self.my_mod.n_sub_carr
+        self.ibo_val_db = self.my_array.array_elements[0].impairment.ibo_db
+        self.n_err_min = n_err_min
+        self.bits_sent_max = bits_sent_max
+        self.device = device
+        self.max_batch = int(max_batch)
+        self._engine = None
+        self._engine_key = None
+        self.set_precoding_and_recalculate_agc()
+
+    # ------------------------------------------------------------------ engine plumbing
+    def _chan_kind(self):
+        if isinstance(self.my_miso_chan, channel.MisoRayleighFd):
+            return "rayleigh"
+        if isinstance(self.my_miso_chan, channel.MisoTwoPathFd):
+            return "two_path"
+        return "los"
+
+    def engine(self, reroll_chan: bool = True):
+        """The configured GPU engine for the current grid point (created lazily, per process)."""
+        kind = self._chan_kind()
+        if kind == "rayleigh" and not reroll_chan:
+            raise NotImplementedError("a fixed Rayleigh realisation (reroll_chan=False) is not supported: "
+                                      "the engine draws every trial's channel on the device")
+        dev = self.device if self.device is not None else _default_device()
+        key = (dev, kind, bool(reroll_chan), self.is_mcnc)
+        if self._engine is None or self._engine_key != key:
+            m = self.my_mod
+            rx = self.my_standard_rx
+            if kind != "rayleigh" and self.rx_loc_y != self.rx_loc_x and not reroll_chan:
+                raise NotImplementedError("fixed LoS RX requires cord_y == cord_x")
+            self._engine = _engine.Engine(
+                self.n_ant_val, m.n_sub_carr, m.n_fft, m.constel_size, m.cp_len, kind,
+                "mcnc" if self.is_mcnc else "cnc", self.my_array.positions(),
+                (self.rx_loc_x, self.rx_loc_y, rx.cord_z), self.rx_loc_var,
+                channel.carrier_freqs(m.n_fft, rx.carrier_spacing, rx.center_freq), reroll=reroll_chan, device=dev)
+            self._engine_key = key
+        self._push_point()
+        return self._engine
+
+    def point_params(self) -> dict:
+        """The per-point scalars the reference keeps in its objects."""
+        kind, sat, p, toi = distortion.pa_params(self.my_array.array_elements[0].impairment)
+        if self.is_mcnc:
+            ck, csat, cp, ctoi, calpha = kind, sat, p, toi, 1.0
+        else:
+            ck, csat, cp, ctoi = distortion.pa_params(self.my_cnc_rx.impairment)
+            calpha = float(self.my_cnc_rx.modem.alpha)
+        return dict(ibo_db=float(self.ibo_val_db), snr_db=float(self.my_noise.snr_db),
+                    avg_symbol_power=float(self.my_mod.avg_symbol_power), pa_kind=kind, sat_pow=sat, p_hardness=p,
+                    toi_coeff=toi, cnc_pa_kind=ck, cnc_sat_pow=csat, cnc_toi_coeff=ctoi, cnc_alpha=calpha,
+                    csi_eps=self.csi_epsylon)
+
+    def _push_point(self):
+        pp = self.point_params()
+        if pp["snr_db"] is None:
+            raise ValueError("set_snr() must be called before simulate()")
+        self._engine.set_point(**pp)
+
+    def __getstate__(self):  # engines (device handles) never travel to another process
+        d = self.__dict__.copy()
+        d["_engine"] = None
+        d["_engine_key"] = None
+        return d
+
+    # ------------------------------------------------------------------ reference API
+    def simulate(self, incl_clean_run: bool, reroll_chan: bool, cnc_n_iter_lst: list, seed_arr: list,
+                 n_err_shared_arr, n_bits_sent_shared_arr) -> None:
+        """Monte-Carlo trial loop on the GPU (mp_model.py:89-228)."""
+        eng = self.engine(reroll_chan)
+        seed = _seed64(seed_arr)
+        iters_all = np.asarray(cnc_n_iter_lst, dtype=np.int64).reshape(-1)
+        order = np.argsort(iters_all, kind="stable")
+        res_idx = 1 if incl_clean_run else 0
+        err_np = np.frombuffer(n_err_shared_arr.get_obj()) if hasattr(n_err_shared_arr, "get_obj") else None
+        trial = 0
+        while True:
+            err = np.asarray(err_np if err_np is not None else n_err_shared_arr[:], dtype=np.float64)
+            bits = np.asarray(n_bits_sent_shared_arr[:], dtype=np.float64)
+            act = (err < self.n_err_min) & (bits < self.bits_sent_max)
+            clean_on = bool(incl_clean_run and act[0])
+            flags = act[res_idx:]
+            if not clean_on and not flags.any():
+                break
+            idx = [res_idx + int(i) for i in order if flags[i]]
+            run_iters = [int(iters_all[i]) for i in order if flags[i]]
+            if not run_iters:  # only the clean counter is still open: the engine always runs iteration 0
+                run_iters, idx = [0], []
+            # one batch never crosses bits_sent_max of the most advanced open counter
+            open_bits = bits[act] if act.any() else bits
+            remaining = max(1.0, self.bits_sent_max - float(np.max(open_bits)))
+            n = int(min(self.max_batch, max(1, np.ceil(remaining / self.n_bits_per_ofdm_sym))))
+            uniq = sorted(set(run_iters))
+            e, b, _ = eng.run(seed, trial, n, uniq, clean_on)
+            trial += n
+            pos = {it: j + (1 if clean_on else 0) for j, it in enumerate(uniq)}
+            lock = n_err_shared_arr.get_lock() if hasattr(n_err_shared_arr, "get_lock") else None
+            if lock:
+                lock.acquire()
+            try:
+                if clean_on:
+                    n_err_shared_arr[0] += float(e[0])
+                    n_bits_sent_shared_arr[0] += float(b[0])
+                for slot, it in zip(idx, [int(iters_all[i]) for i in order if flags[i]]):
+                    n_err_shared_arr[slot] += float(e[pos[it]])
+                    n_bits_sent_shared_arr[slot] += float(b[pos[it]])
+            finally:
+                if lock:
+                    lock.release()
+
+    def update_distortion(self, ibo_val_db: float) -> None:
+        """(mp_model.py:230-241)"""
+        self.my_array.update_distortion(ibo_db=ibo_val_db, avg_sample_pow=self.my_mod.avg_sample_power)
+        if isinstance(self.my_cnc_rx, corrector.CncReceiver):
+            self.my_cnc_rx.update_distortion(ibo_db=ibo_val_db)
+        self.ibo_val_db = self.my_array.array_elements[0].impairment.ibo_db
+        self.recalculate_agc(ak_part_only=True)
+
+    def set_snr(self, snr_db_val: float) -> None:
+        """(mp_model.py:243-251)"""
+        self.my_noise.snr_db = float(snr_db_val)
+
+    def set_precoding_and_recalculate_agc(self) -> None:
+        """(mp_model.py:253-288) for the object state (the engine redoes it per trial on the device)."""
+        h = self.my_miso_chan.channel_mat_fd
+        if self.csi_epsylon is not None:
+            n_sc = self.my_mod.n_sub_carr
+            noisy = np.copy(h)
+            for r, row in enumerate(noisy):
+                sc = np.concatenate((row[-n_sc // 2:], row[1:(n_sc // 2) + 1]))
+                pw = np.sum(np.abs(sc) ** 2) / len(sc)
+                z = self.my_noise.rng_gen.standard_normal((len(sc), 2)).view(np.complex128)[:, 0]
+                nsc = np.sqrt(1 - self.csi_epsylon ** 2) * sc + z * 0.5 * np.sqrt(2 * pw) * self.csi_epsylon
+                noisy[r, -(n_sc // 2):] = nsc[:n_sc // 2]
+                noisy[r, 1:(n_sc // 2) + 1] = nsc[n_sc // 2:]
+            self.my_miso_chan_csi_err.channel_mat_fd = noisy
+            h = noisy
+        self.my_array._set_mrt_state(h)
+        self.recalculate_agc(channel_mat_fd=h)
+
+    def recalculate_agc(self, channel_mat_fd: ndarray = None, ak_part_only: bool = False) -> None:
+        """(mp_model.py:290-329)"""
+        n_sc = self.n_sub_carr
+        if not ak_part_only:
+            hk = sc_columns(channel_mat_fd, n_sc)
+            vk = self.my_array.get_precoding_mat()
+            self.vk_pow_vec = np.sum(np.abs(vk) ** 2, axis=1)
+            self.hk_vk_agc = hk * vk
+            g = np.sum(self.hk_vk_agc, axis=0)
+            self.hk_vk_noise_scaler = np.mean(np.abs(g) ** 2)
+            self.hk_vk_agc_nfft = np.ones(self.my_mod.n_fft, dtype=np.complex128)
+            self.hk_vk_agc_nfft[-(n_sc // 2):] = g[:n_sc // 2]
+            self.hk_vk_agc_nfft[1:(n_sc // 2) + 1] = g[n_sc // 2:]
+            self.my_array.update_distortion(ibo_db=self.ibo_val_db, avg_sample_pow=self.my_mod.avg_sample_power)
+            if isinstance(self.my_cnc_rx, corrector.CncReceiver):
+                self.my_cnc_rx.update_distortion(ibo_db=self.ibo_val_db)
+        ibo_vec = 10 * np.log10(10 ** (self.ibo_val_db / 10) * self.my_mod.n_sub_carr / (self.vk_pow_vec * self.n_ant_val))
+        ak = np.expand_dims(self.my_mod.calc_alpha(ibo_db=ibo_vec), axis=1)
+        g = np.sum(ak * self.hk_vk_agc, axis=0)
+        self.ak_hk_vk_noise_scaler = np.mean(np.abs(g) ** 2)
+        self.ak_hk_vk_agc_nfft = np.ones(self.my_mod.n_fft, dtype=np.complex128)
+        self.ak_hk_vk_agc_nfft[-(n_sc // 2):] = g[:n_sc // 2]
+        self.ak_hk_vk_agc_nfft[1:(n_sc // 2) + 1] = g[n_sc // 2:]
+        if isinstance(self.my_cnc_rx, corrector.McncReceiver):
+            self.my_cnc_rx.agc_corr_vec = self.ak_hk_vk_agc_nfft

@@ -1,0 +1,62 @@
+"""Link.simulate drop-in on the GPU: counter semantics, equality with the engine, BER
+sanity against closed form (BASELINE config 1 plumbing) and the reference's CSV point."""
+import ctypes
+import multiprocessing as mp
+
+import numpy as np
+import pytest
+from scipy import special
+
+from link_util import build_link
+
+pytestmark = pytest.mark.gpu
+
+
+def shared(n):
+    return mp.Array(ctypes.c_double, n, lock=True), mp.Array(ctypes.c_double, n, lock=True)
+
+
+def test_simulate_equals_engine():
+    link, mod = build_link(n_ant=8, n_sc=256, n_fft=512, M=16, ibo=1.0, bits_sent_max=1024 * 300,
+                           n_err_min=10 ** 12)
+    link.set_snr(14.0)
+    err, bits = shared(4)
+    link.simulate(True, True, np.array([0, 1, 2]), [11, 22, 33], err, bits)
+    from mp_model import _seed64
+    eng = link.engine()
+    e, b, _ = eng.run(_seed64([11, 22, 33]), 0, 300, [0, 1, 2], True)
+    np.testing.assert_array_equal(np.asarray(err[:]), e.astype(float))
+    np.testing.assert_array_equal(np.asarray(bits[:]), b.astype(float))
+
+
+@pytest.mark.parametrize("ebn0", [4.0, 8.0, 10.0])
+def test_config1_siso_awgn_vs_theory(ebn0):
+    """BASELINE config 1: 1 antenna, 64 sc / FFT 128, 16-QAM, ideal PA, LoS (|H| ~ const).
+    Gray 16-QAM: BER = 3/8 erfc(sqrt(0.4 Eb/N0)); 1e5+ bits."""
+    from utilities import ebn0_to_snr
+    link, mod = build_link(n_ant=1, n_sc=64, n_fft=128, M=16, ibo=100.0, chan="los", bits_sent_max=256 * 2000)
+    link.set_snr(float(ebn0_to_snr(ebn0, 64, 64, 16)))
+    err, bits = shared(2)
+    link.simulate(True, True, np.array([0]), [1, 2, 3], err, bits)
+    theory = 3 / 8 * special.erfc(np.sqrt(0.4 * 10 ** (ebn0 / 10)))
+    ber = np.asarray(err[:]) / np.asarray(bits[:])
+    sigma = np.sqrt(theory * 4 / bits[0]) + 1e-6
+    assert abs(ber[0] - theory) < 6 * sigma, (ber, theory)
+    assert abs(ber[1] - theory) < 6 * sigma, (ber, theory)
+
+
+def test_published_csv_point_rayleigh():
+    """Paper config (64 ant, N_fft 4096, 2048 sc, 64-QAM, IBO 3, Eb/N0 15, Rayleigh):
+    published BER no-dist 9.368e-4, std RX 1.076e-3, CNC-1 2.794e-2
+    (figs/csv_results/ber_vs_ebn0_cnc_rayleigh_nant64_ibo3_..._niter1_..._8.csv col 11)."""
+    from utilities import ebn0_to_snr
+    link, mod = build_link(n_ant=64, n_sc=2048, n_fft=4096, M=64, cp=128, ibo=3.0, bits_sent_max=12288 * 2048)
+    link.set_snr(float(ebn0_to_snr(15.0, 2048, 2048, 64)))
+    err, bits = shared(3)
+    link.simulate(True, True, np.array([0, 1]), [7, 8, 9], err, bits)
+    ber = np.asarray(err[:]) / np.asarray(bits[:])
+    pub = np.array([9.368e-4, 1.076e-3, 2.794e-2])
+    # batch-means-free bound: errors are clustered per symbol, allow 6 binomial sigma x 3 (cluster factor)
+    sig = np.sqrt(pub / bits[0]) * 3
+    print("paper-config BER", ber, "published", pub)
+    assert np.all(np.abs(ber - pub) < 6 * sig + 0.03 * pub), (ber, pub)

@@ -1,0 +1,130 @@
+"""CPU tests of the Link drop-in's host logic (no GPU): object state vs the reference's,
+HIP-free construction, the stopping rule and counter layout (mp_model.py:133-222), with a
+fake engine standing in for libmimo_engine."""
+import ctypes
+import multiprocessing as mp
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from link_util import build_link
+from oracle import refmath as rm
+
+
+class FakeEngine:
+    """Deterministic stand-in: every trial has `e` errors at every index."""
+
+    def __init__(self, bits_per_trial, errs_per_trial=3):
+        self.calls = []
+        self.bpt = bits_per_trial
+        self.e = errs_per_trial
+
+    def run(self, seed, first, n, iters, incl_clean, per_trial=False):
+        self.calls.append((seed, first, n, tuple(iters), incl_clean))
+        k = len(iters) + (1 if incl_clean else 0)
+        return (np.full(k, self.e * n, np.uint64), np.full(k, self.bpt * n, np.uint64), None)
+
+
+def shared(n):
+    return mp.Array(ctypes.c_double, n, lock=True), mp.Array(ctypes.c_double, n, lock=True)
+
+
+def test_link_state_matches_reference_objects(units):
+    """Precoding / PA calibration / AGC attributes equal the reference's for the same H."""
+    link, mod = build_link(n_ant=4, n_sc=64, n_fft=128, M=16, ibo=2.0)
+    link.my_miso_chan.channel_mat_fd = units["arr_H"]
+    link.set_precoding_and_recalculate_agc()
+    np.testing.assert_allclose(link.my_array.get_precoding_mat(), units["arr_P"], rtol=1e-12)
+    np.testing.assert_allclose([e.impairment.sat_pow for e in link.my_array.array_elements], units["arr_sat"],
+                               rtol=1e-12)
+    np.testing.assert_allclose(link.ak_hk_vk_agc_nfft, units["arr_ak_agc"], rtol=1e-12)
+    np.testing.assert_allclose(link.hk_vk_agc_nfft, units["arr_hk_agc"], rtol=1e-12)
+    assert link.ak_hk_vk_noise_scaler == pytest.approx(float(units["arr_ak_noise"]), rel=1e-12)
+    pp = link.point_params()
+    assert pp["cnc_alpha"] == pytest.approx(float(units["cnc_alpha"]), rel=1e-14)
+    assert pp["cnc_sat_pow"] == pytest.approx(float(units["cnc_sat"]), rel=1e-14)
+
+
+def test_point_params_config2():
+    link, mod = build_link(n_ant=64, n_sc=1024, n_fft=2048, M=64, cp=128, ibo=3.0)
+    link.set_snr(float(rm.ebn0_to_snr(15, 1024, 1024, 64)))
+    pp = link.point_params()
+    # sat = 10^(IBO/10) * Es * S/F * mean|P|^2 with mean|P|^2 = 1/A (antenna_array.py:328-360)
+    assert pp["sat_pow"] == pytest.approx(10 ** 0.3 * 42 * 0.5 / 64, rel=1e-12)
+    assert pp["cnc_sat_pow"] == pytest.approx(41.9005086, rel=1e-7)
+    assert pp["cnc_alpha"] == pytest.approx(0.9213017188, rel=1e-9)
+    assert pp["avg_symbol_power"] == pytest.approx(42.0)
+
+
+def test_stopping_rule_bits_budget(monkeypatch):
+    link, mod = build_link(bits_sent_max=256 * 40, n_err_min=10 ** 9)
+    fake = FakeEngine(mod.n_bits_per_ofdm_sym)
+    monkeypatch.setattr(link, "engine", lambda reroll=True: fake)
+    err, bits = shared(1 + 3)
+    link.simulate(True, True, np.array([0, 1, 2]), [1, 2, 3], err, bits)
+    assert list(bits[:]) == [256 * 40] * 4          # exactly the budget, no overshoot
+    assert list(err[:]) == [3 * 40] * 4
+    assert sum(c[2] for c in fake.calls) == 40
+    firsts = [c[1] for c in fake.calls]
+    assert firsts == sorted(firsts) and firsts[0] == 0   # trial ids advance, never reused
+
+
+def test_stopping_rule_per_index(monkeypatch):
+    """Indices that reached n_err_min stop accumulating; the others continue (mp_model.py:181-187)."""
+    link, mod = build_link(bits_sent_max=10 ** 9, n_err_min=300, max_batch=16)
+
+    class Skewed(FakeEngine):
+        def run(self, seed, first, n, iters, incl_clean, per_trial=False):
+            self.calls.append((seed, first, n, tuple(iters), incl_clean))
+            e = [(10 if it == 0 else 1) * n for it in iters]
+            if incl_clean:
+                e = [1 * n] + e
+            return np.asarray(e, np.uint64), np.full(len(e), self.bpt * n, np.uint64), None
+
+    fake = Skewed(mod.n_bits_per_ofdm_sym)
+    monkeypatch.setattr(link, "engine", lambda reroll=True: fake)
+    err, bits = shared(3)
+    link.simulate(True, True, np.array([0, 4]), [5], err, bits)
+    assert err[1] >= 300 and err[1] < 300 + 10 * 16      # iteration 0 stopped early
+    assert err[0] >= 300 and err[2] >= 300
+    assert bits[1] < bits[2]                            # ... while iteration 4 kept running
+    assert all(set(c[3]) <= {0, 4} for c in fake.calls)
+
+
+def test_seed_derivation_distinct():
+    from mp_model import _seed64
+    assert _seed64([1, 2, 3]) != _seed64([1, 2, 4])
+    assert _seed64([1, 2, 3]) == _seed64(np.array([1, 2, 3]))
+
+
+def test_link_construction_is_hip_free(monkeypatch):
+    """Drivers fork after building Link: construction / update_distortion / set_snr must not call HIP."""
+    import _engine
+
+    def boom(*a, **k):
+        raise AssertionError("HIP touched during Link construction")
+
+    monkeypatch.setattr(_engine, "lib", boom)
+    link, _ = build_link(is_mcnc=True)
+    link.update_distortion(2.0)
+    link.set_snr(12.0)
+    link2, _ = build_link(csi=0.2)
+    link2.set_precoding_and_recalculate_agc()
+
+
+def test_link_pickles_without_engine():
+    import pickle
+    link, _ = build_link()
+    link._engine = object()
+    state = pickle.loads(pickle.dumps(link.__getstate__()))
+    assert state["_engine"] is None
+
+
+def test_unsupported_channels_raise():
+    import mp_model
+    with pytest.raises(NotImplementedError):
+        link, _ = build_link()
+        link._chan_kind = lambda: "rayleigh"
+        link.device = 0
+        link.engine(reroll_chan=False)
