@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmimo_engine.so")
+LIB_PATH = os.environ.get("MIMO_LIB") or os.path.join(_HERE, "libmimo_engine.so")
 
 PA_KINDS = {"none": 0, "softlim": 1, "rapp": 2, "toi": 3}
 CH_KINDS = {"rayleigh": 1, "los": 2, "two_path": 3}

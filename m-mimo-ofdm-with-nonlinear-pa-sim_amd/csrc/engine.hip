@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -85,6 +86,10 @@ mimo::InstanceKey select_instance(const mimo_engine* e, bool csi) {
   mimo::InstanceKey k{};
   k.F = e->cfg.n_fft;
   k.T = team_for(k.F);
+  if (const char* env = std::getenv("MIMO_TEAM")) {  // A/B override: MIMO_TEAM=<threads per trial>
+    const int t = std::atoi(env);
+    if (t == mimo::alt_team_size(k.F) || t == mimo::team_size(k.F)) k.T = t;
+  }
   const int S = e->cfg.n_sub_carr;
   const int P = k.F / k.T;
   k.aligned = (S % (4 * k.T) == 0) && S < k.F && (S / k.T == 8 || S / k.T == 4) && (S / k.T) < P;
@@ -95,6 +100,11 @@ mimo::InstanceKey select_instance(const mimo_engine* e, bool csi) {
 }
 
 hipError_t launch(const mimo::InstanceKey& k, dim3 grid, hipStream_t st, const mimo::TrialParams& p, bool* found) {
+#ifdef MIMO_ONLY_F2048
+  if (k.F == 2048) return mimo::launch_trial_F2048(k, grid, st, p, found);
+  *found = false;
+  return hipSuccess;
+#endif
   switch (k.F) {
     case 128: return mimo::launch_trial_F128(k, grid, st, p, found);
     case 256: return mimo::launch_trial_F256(k, grid, st, p, found);
@@ -285,6 +295,10 @@ int32_t mimo_engine_run(mimo_engine* e, uint64_t seed, uint64_t first_trial, uin
   p.rx_z = c.rx_pos[2];
   p.rx_var = c.reroll_chan ? c.rx_loc_var : 0.0;
   p.d0 = e->d0;
+  p.ablate = 0;
+#ifdef MIMO_ABLATION
+  if (const char* env = std::getenv("MIMO_ABLATE")) p.ablate = (uint32_t)std::strtoul(env, nullptr, 0);
+#endif
   if (!c.reroll_chan && c.channel_kind != MIMO_CH_RAYLEIGH) {
     // fixed RX: jitter span 0 around (x0, x0); only consistent when rx_y == rx_x
     if (c.rx_pos[1] != c.rx_pos[0]) return fail(MIMO_EINVAL, "reroll_chan=0 requires rx_pos[1] == rx_pos[0]");

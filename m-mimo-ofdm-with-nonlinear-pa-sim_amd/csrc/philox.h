@@ -23,6 +23,9 @@ struct Key {
   uint32_t k0, k1;
 };
 
+// One round = 2 x v_mad_u64_u32 (the full 64-bit product in one ~4-cycle wave64
+// instruction) + 4 x v_xor_b32, instead of mul_hi + mul_lo per word: every 32-bit integer
+// op is half rate on gfx950 (tools/microbench/ops.hip); gfx950 has no v_xor3_b32.
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, Key key) {
   uint32_t k0 = key.k0, k1 = key.k1;
 #pragma unroll
@@ -31,11 +34,9 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, Key key) {
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
     }
-    const uint32_t lo0 = 0xD2511F53u * c.x;
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z);
-    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0);
   }
   return c;
 }

@@ -8,10 +8,12 @@
 // register e / T).  A Stockham autosort radix-R stage reads, for butterfly
 // j = t + T*i, the elements j + r*F/R = t + T*(i + r*P/R): all in the thread's own
 // registers.  The last stage writes j + r*F/R as well, so input and output are both
-// cyclic and a transform needs (stages - 1) exchanges through a padded LDS buffer
+// cyclic and a transform needs (stages - 1) exchanges through padded LDS buffers
 // (one pad slot per 32 elements: conflict-free ds_write_b64 / ds_read_b64 for the
 // stage patterns used here).  F = 2048 with P = 16 is radix 16 x 16 x 8: two
-// exchanges, four barriers.
+// exchanges, two barriers.
+//
+// Two alternating exchange buffers: one barrier per exchange (see stage()).
 //
 // Scaling is left to the caller (transforms are un-normalised).  DIR = -1 forward
 // (e^{-j2pi nk/F}), +1 inverse.
@@ -137,14 +139,21 @@ struct TeamFft {
   static constexpr int bits_before(int s) { return s == 0 ? 0 : bits_before(s - 1) + bits(s - 1); }
   static __device__ __forceinline__ int pad(int e) { return e + (e >> 5); }
 
-  template <int S, int DIR>
-  static __device__ __forceinline__ void stage(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t) {
+  // Exchange buffers alternate (stage S of a transform started at parity PAR uses buffer
+  // (S + PAR) & 1), so a write never targets the buffer other threads may still be
+  // reading: before a thread writes buffer X for exchange k+2 it has passed the barrier
+  // of exchange k+1, which every thread reaches only after reading X for exchange k.
+  // One barrier per exchange.  Callers keep the number of exchanges between two
+  // transforms' parities consistent (an antenna = IFFT + FFT = an even count).
+  template <int S, int DIR, int PAR>
+  static __device__ __forceinline__ void stage(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
+                                               bool no_xchg) {
     constexpr int R = 1 << bits(S);
     constexpr int NS = 1 << bits_before(S);
     constexpr int B = P / R;
     constexpr bool LAST = (S == NST - 1);
     static_assert(B >= 1 && B * R == P, "radix must divide points per thread");
-    if constexpr (!LAST) __syncthreads();  // every thread has read the previous exchange
+    float2* buf = lds + ((S + PAR) & 1) * LDS_ELEMS;
 #pragma unroll
     for (int i = 0; i < B; ++i) {
       float2 v[R];
@@ -164,26 +173,35 @@ struct TeamFft {
       if constexpr (LAST) {
 #pragma unroll
         for (int r = 0; r < R; ++r) d[i + r * B] = v[r];
+      } else if (no_xchg) {  // ablation: data stay in registers (wrong result, no LDS / barriers)
+#pragma unroll
+        for (int r = 0; r < R; ++r) d[i + r * B] = v[r];
       } else {
         const int base = (j / NS) * NS * R + jm;
 #pragma unroll
-        for (int r = 0; r < R; ++r) lds[pad(base + r * NS)] = v[r];
+        for (int r = 0; r < R; ++r) buf[pad(base + r * NS)] = v[r];
       }
     }
     if constexpr (!LAST) {
-      __syncthreads();
+      if (!no_xchg) {
+        __syncthreads();
 #pragma unroll
-      for (int m = 0; m < P; ++m) d[m] = lds[pad(t + T * m)];
+        for (int m = 0; m < P; ++m) d[m] = buf[pad(t + T * m)];
+      }
     }
   }
 
-  template <int S, int DIR>
-  static __device__ __forceinline__ void stages(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t) {
+  template <int S, int DIR, int PAR>
+  static __device__ __forceinline__ void stages(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
+                                                bool no_xchg) {
     if constexpr (S < NST) {
-      stage<S, DIR>(d, lds, tw, t);
-      stages<S + 1, DIR>(d, lds, tw, t);
+      stage<S, DIR, PAR>(d, lds, tw, t, no_xchg);
+      stages<S + 1, DIR, PAR>(d, lds, tw, t, no_xchg);
     }
   }
+
+  static constexpr int XCHG = NST - 1;  // exchanges per transform
+  static constexpr int LDS_TOTAL = 2 * LDS_ELEMS;  // two exchange buffers
 
   // Un-normalised transform of the team's cyclic-distributed vector.  Ends with the
   // last exchange's reads done by this thread only: callers that touch `lds` next must
@@ -193,13 +211,20 @@ struct TeamFft {
   // caller's antenna loop LICM would hoist all of them (~60 VGPRs) out of the loop and
   // spill.  Laundering t and tw through empty asm makes them opaque per transform:
   // they are re-derived (cheap ALU + L1-hit loads) instead of held.
-  template <int DIR>
-  static __device__ __forceinline__ void run(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t) {
+  template <int DIR, int PAR = 0>
+  static __device__ __forceinline__ void run(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
+                                             bool no_xchg = false) {
     const float2* twl = tw;
     int tl = t;
     asm volatile("" : "+s"(twl));
     asm volatile("" : "+v"(tl));
-    stages<0, DIR>(d, lds, twl, tl);
+    stages<0, DIR, PAR>(d, lds, twl, tl, no_xchg);
+  }
+  // IFFT then FFT of one antenna / CNC iteration: an even number of exchanges in total.
+  template <int DIR>
+  static __device__ __forceinline__ void run_second(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
+                                                    bool no_xchg = false) {
+    run<DIR, XCHG & 1>(d, lds, tw, t, no_xchg);
   }
 };
 

@@ -56,7 +56,17 @@ struct TrialParams {
   uint32_t rec_mask;             // bit i: record iteration i
   int incl_clean, n_idx;
   double rx_x0, rx_z, rx_var, d0; // LoS / two-path geometry
+  uint32_t ablate;               // diagnostic builds only (-DMIMO_ABLATION), see ABL_* below
 };
+
+// Ablation switches for cost breakdowns.  Compiled in only with -DMIMO_ABLATION
+// (libmimo_engine_ablation.so); the production kernel has none of these branches.
+enum : uint32_t { ABL_RNG = 1, ABL_FFT = 2, ABL_PASS1 = 4, ABL_PA = 8, ABL_XCHG = 16 };
+#ifdef MIMO_ABLATION
+#define MIMO_ABL(p, bit) (((p).ablate & (bit)) != 0)
+#else
+#define MIMO_ABL(p, bit) false
+#endif
 
 // ---------------------------------------------------------------- slot geometry
 // ALIGNED: S % (4T) == 0 and S < F.  Slot s < HALF is the positive band (bin
@@ -243,7 +253,13 @@ struct Channel {
                                              const double (&rx)[3], float2 (&h)[NSLOT]) {
     const int S = p.n_sc;
     if constexpr (CH == CH_RAYLEIGH) {
-      normals(key, trial, ST_CHAN, (uint32_t)a, t, S, h);
+      if (MIMO_ABL(p, ABL_RNG)) {
+#pragma unroll
+        for (int s = 0; s < NSLOT; ++s)
+          h[s] = make_float2(1.0f + 1e-3f * (float)((a + s + t) & 7), 0.5f - 1e-3f * (float)((a * s) & 3));
+      } else {
+        normals(key, trial, ST_CHAN, (uint32_t)a, t, S, h);
+      }
       const float sa = p.ant_rel[a];
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
@@ -302,7 +318,7 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
   constexpr int P = FFT::P;
   constexpr int W = T / 64;
 
-  __shared__ float2 lds[FFT::LDS_ELEMS];
+  __shared__ float2 lds[FFT::LDS_TOTAL];
   __shared__ float red[kMaxWaves];
   __shared__ float vk_part[2][kMaxWaves];
   __shared__ float pw_csi[CSI ? 1024 : 1];
@@ -340,7 +356,7 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
   float nrm2[NSLOT];
 #pragma unroll
   for (int s = 0; s < NSLOT; ++s) nrm2[s] = 0.f;
-  for (int a = 0; a < A; ++a) {
+  for (int a = 0; a < (MIMO_ABL(p, ABL_PASS1) ? 1 : A); ++a) {
     const int tl = opaque(t);
     float2 h[NSLOT];
     CHN::gen(p, key, trial, a, tl, rx, h);
@@ -428,11 +444,14 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
         if (lane == 0) vk_part[a & 1][wid] = vk;  // read after the IFFT's first barrier
       }
       SL::scatter(d, x, t0);
-      FFT::template run<+1>(d, lds, p.tw, t);
+      if (!MIMO_ABL(p, ABL_FFT)) FFT::template run<+1>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG));
+      if (!MIMO_ABL(p, ABL_PA)) {
 #pragma unroll
-      for (int m = 0; m < P; ++m)
-        d[m] = pa_apply(p.pa_kind, d[m], p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
-      FFT::template run<-1>(d, lds, p.tw, t);
+        for (int m = 0; m < P; ++m)
+          d[m] = pa_apply(p.pa_kind, d[m], p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
+      }
+      if (!MIMO_ABL(p, ABL_FFT)) FFT::template run_second<-1>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG));
+      if (MIMO_ABL(p, ABL_FFT)) __syncthreads();  // keep the vk_part hand-off ordered
       float alpha_a = 0.f;
       if (main_pass) {
         float vks = 0.f;
@@ -525,7 +544,7 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
 #pragma unroll
       for (int m = 0; m < P; ++m)
         d[m] = pa_apply(p.cnc_pa_kind, d[m], p.sat_cnc, p.sqrt_sat_cnc, p.inv_sat_cnc, p.rapp_p, p.toi_cnc);
-      FFT::template run<-1>(d, lds, p.tw, t);
+      FFT::template run_second<-1>(d, lds, p.tw, t);
       const float sc = inv_sqrt_f * p.inv_alpha_cnc;
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {

@@ -8,6 +8,9 @@ namespace mimo {
 
 // Team (workgroup) size per FFT size: 16 points per thread from F = 1024 up, one wave below.
 constexpr int team_size(int F) { return F >= 1024 ? F / 16 : 64; }
+// Alternative team (8 points per thread: half the registers, 2x the waves, one more
+// LDS exchange per transform), selectable with MIMO_TEAM=<T> for A/B measurements.
+constexpr int alt_team_size(int F) { return F >= 1024 ? F / 8 : team_size(F); }
 
 struct InstanceKey {
   int F, T, nslot;
