@@ -1,0 +1,205 @@
+"""Grid sweeps over (IBO, Eb/N0) points, sharded across GPUs (BASELINE config 4).
+
+Replaces the outer loops of the reference drivers (e.g.
+``main_mp_miso_cnc_ber_vs_ebn0.py:97-141``,
+``main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:100-215``), which run every grid point
+on one host with ``num_cores`` forked ``Link.simulate`` processes and shared counters.
+
+MI355X design: one process per GPU (torchrun; ``torch.distributed`` with the ``nccl``
+backend = RCCL over xGMI).  Grid points are independent, so they are dealt round-robin
+over ranks with no data-path communication; each point's Philox seed is derived from its
+grid index, so results do not depend on the number of GPUs.  The only collective is one
+all-reduce of the int64 counter tensor [points, indices, {errors, bits}] at the end (a
+few KB: latency-bound, one message).  Rank 0 then forms BERs and writes the reference's
+CSV layouts (``docs/source/usage.rst:40-56``).
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 sweep.py --grid fixed_ber ...
+"""
+from __future__ import annotations
+
+import argparse
+import os
+
+import numpy as np
+
+from utilities import ebn0_to_snr, save_to_csv
+
+
+def point_seed(base_seed: int, point_index: int) -> list:
+    """Seed array of one grid point (fed to Link.simulate, which hashes it)."""
+    return [int(base_seed) & 0x7FFFFFFFFFFFFFFF, int(point_index), 0x5EED]
+
+
+def owned_points(n_points: int, rank: int, world: int) -> list:
+    return list(range(rank, n_points, world))
+
+
+def run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean=True, seed=2137, rank=0, world=1, dist=None,
+             device=None, reroll_chan=True):
+    """Simulate every (IBO, Eb/N0) point this rank owns; all-reduce the counters.
+
+    Returns (err, bits) int64 arrays of shape [n_ibo, n_ebn0, n_idx] on every rank.
+    ``link`` is a ``mp_model.Link``-like object (update_distortion / set_snr / simulate).
+    """
+    ibo_arr = np.asarray(ibo_arr, dtype=np.float64)
+    ebn0_arr = np.asarray(ebn0_arr, dtype=np.float64)
+    iters = np.asarray(iters)
+    n_idx = len(iters) + (1 if incl_clean else 0)
+    n_pts = len(ibo_arr) * len(ebn0_arr)
+    counts = np.zeros((n_pts, n_idx, 2), dtype=np.int64)
+    m = link.my_mod
+    current_ibo = None
+    for p in owned_points(n_pts, rank, world):
+        i_ibo, i_snr = divmod(p, len(ebn0_arr))
+        if current_ibo != ibo_arr[i_ibo]:
+            link.update_distortion(ibo_val_db=float(ibo_arr[i_ibo]))
+            current_ibo = ibo_arr[i_ibo]
+        # drivers convert with n_fft = n_sub_carr (main_mp_miso_cnc_ber_vs_ebn0.py:112)
+        link.set_snr(float(ebn0_to_snr(ebn0_arr[i_snr], m.n_sub_carr, m.n_sub_carr, m.constel_size)))
+        err = np.zeros(n_idx)
+        bits = np.zeros(n_idx)
+        link.simulate(incl_clean, reroll_chan, iters, point_seed(seed, p), err, bits)
+        counts[p, :, 0] = err.astype(np.int64)
+        counts[p, :, 1] = bits.astype(np.int64)
+    if dist is not None and world > 1:
+        import torch
+        dev = torch.device(f"cuda:{device}") if device is not None and dist.get_backend() == "nccl" else None
+        t = torch.from_numpy(counts).to(dev) if dev is not None else torch.from_numpy(counts)
+        dist.all_reduce(t)  # each point is filled by exactly one rank: SUM == gather
+        counts = t.cpu().numpy()
+    counts = counts.reshape(len(ibo_arr), len(ebn0_arr), n_idx, 2)
+    return counts[..., 0], counts[..., 1]
+
+
+def ber_from_counts(err, bits):
+    """BER with NaN where nothing was sent (main_mp_miso_cnc_ber_vs_ebn0.py:134-139)."""
+    err = np.asarray(err, dtype=np.float64)
+    bits = np.asarray(bits, dtype=np.float64)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        return np.where(bits == 0, np.nan, err / np.where(bits == 0, 1, bits))
+
+
+def required_ebn0(ber_per_ibo_snr_iter, ebn0_arr, target_ber):
+    """Eb/N0 reaching ``target_ber`` per (iteration, IBO) by linear interpolation of Eb/N0
+    over BER, inf where the target is outside the measured range
+    (main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:151-180)."""
+    from scipy import interpolate
+    n_ibo, _, n_it = ber_per_ibo_snr_iter.shape
+    out = np.zeros((n_it, n_ibo))
+    for it in range(n_it):
+        for ib in range(n_ibo):
+            f = interpolate.interp1d(ber_per_ibo_snr_iter[ib, :, it], ebn0_arr)
+            try:
+                out[it, ib] = f(target_ber)
+            except ValueError:
+                out[it, ib] = np.inf
+    return out
+
+
+def ber_vs_ebn0_rows(ebn0_arr, ber_idx_by_snr):
+    """CSV rows: x axis, then one row per counter index (usage.rst:40-56)."""
+    return [np.asarray(ebn0_arr)] + [np.asarray(r) for r in ber_idx_by_snr]
+
+
+def fixed_ber_rows(ibo_arr, ber_per_ibo_snr_iter):
+    """CSV rows of the fixed-BER grid: IBO axis, then IBO-major x Eb/N0 rows of per-iteration
+    BERs (main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:208-213)."""
+    rows = [np.asarray(ibo_arr)]
+    for per_snr in ber_per_ibo_snr_iter:
+        for per_it in per_snr:
+            rows.append(np.asarray(per_it))
+    return rows
+
+
+def _build_link(args, device):
+    import copy
+
+    import antenna_array
+    import channel
+    import distortion
+    import modulation
+    import mp_model
+    import noise
+    import transceiver
+
+    mod = modulation.OfdmQamModem(constel_size=args.qam, n_fft=args.n_fft, n_sub_carr=args.n_sc, cp_len=args.cp)
+    if args.pa == "rapp":
+        dist_obj = distortion.Rapp(ibo_db=0, p_hardness=args.p_hardness, avg_samp_pow=mod.avg_sample_power)
+    else:
+        dist_obj = distortion.SoftLimiter(0, mod.avg_sample_power)
+    tx = transceiver.Transceiver(modem=copy.deepcopy(mod), impairment=copy.deepcopy(dist_obj), center_freq=int(3.5e9),
+                                 carrier_spacing=int(15e3))
+    rx = transceiver.Transceiver(modem=copy.deepcopy(mod), impairment=copy.deepcopy(dist_obj), cord_x=212.0,
+                                 cord_y=212.0, cord_z=1.5, center_freq=int(3.5e9), carrier_spacing=int(15e3))
+    arr = antenna_array.LinearArray(n_elements=args.n_ant, base_transceiver=tx, center_freq=int(3.5e9),
+                                    wav_len_spacing=0.5, cord_x=0, cord_y=0, cord_z=15)
+    if args.channel == "rayleigh":
+        ch = channel.MisoRayleighFd(tx_transceivers=arr.array_elements, rx_transceiver=rx, seed=1234)
+    else:
+        ch = channel.MisoLosFd() if args.channel == "los" else channel.MisoTwoPathFd()
+        ch.calc_channel_mat(tx_transceivers=arr.array_elements, rx_transceiver=rx, skip_attenuation=False)
+    return mp_model.Link(mod_obj=mod, array_obj=arr, std_rx_obj=rx, chan_obj=ch, noise_obj=noise.Awgn(snr_db=10),
+                         rx_loc_var=10.0, n_err_min=args.n_err_min, bits_sent_max=args.bits_sent_max,
+                         is_mcnc=args.receiver == "mcnc", device=device)
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--grid", choices=["ber_vs_ebn0", "fixed_ber"], default="fixed_ber")
+    ap.add_argument("--n-ant", type=int, default=64)
+    ap.add_argument("--n-sc", type=int, default=2048)
+    ap.add_argument("--n-fft", type=int, default=4096)
+    ap.add_argument("--cp", type=int, default=128)
+    ap.add_argument("--qam", type=int, default=64)
+    ap.add_argument("--pa", choices=["softlim", "rapp"], default="softlim")
+    ap.add_argument("--p-hardness", type=float, default=3.0)
+    ap.add_argument("--channel", choices=["rayleigh", "los", "two_path"], default="rayleigh")
+    ap.add_argument("--receiver", choices=["cnc", "mcnc"], default="cnc")
+    ap.add_argument("--ibo", type=str, default="0:8:0.5", help="start:stop:step (numpy arange)")
+    ap.add_argument("--ebn0", type=str, default="10:23.1:0.5")
+    ap.add_argument("--iters", type=str, default="0,1,2,3,4,5,6,7,8")
+    ap.add_argument("--target-ber", type=float, default=1e-2)
+    ap.add_argument("--bits-sent-max", type=int, default=int(5e6))
+    ap.add_argument("--n-err-min", type=int, default=int(1e5))
+    ap.add_argument("--seed", type=int, default=2137)
+    ap.add_argument("--out", type=str, default="figs/csv_results")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    rng = lambda s: np.arange(*[float(x) for x in s.split(":")])  # noqa: E731
+    ibo_arr, ebn0_arr = rng(args.ibo), rng(args.ebn0)
+    iters = np.asarray([int(x) for x in args.iters.split(",")])
+    incl_clean = args.grid == "ber_vs_ebn0"
+    link = _build_link(args, local)
+    err, bits = run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean, args.seed, rank, world, dist, local)
+    if rank == 0:
+        ber = ber_from_counts(err, bits)
+        tag = "%s_%s_nant%d" % (args.receiver, args.channel, args.n_ant)
+        if args.grid == "fixed_ber":
+            name = "fixed_ber%1.1e_%s_ebn0_min%d_max%d_step%1.2f_ibo_min%d_max%d_step%1.2f_niter%s" % (
+                args.target_ber, tag, min(ebn0_arr), max(ebn0_arr), ebn0_arr[1] - ebn0_arr[0], min(ibo_arr),
+                max(ibo_arr), ibo_arr[1] - ibo_arr[0], "_".join(str(v) for v in iters[1:]))
+            save_to_csv(fixed_ber_rows(ibo_arr, ber), name, directory=args.out)
+            req = required_ebn0(ber, ebn0_arr, args.target_ber)
+            save_to_csv([ibo_arr] + list(req), "req_ebn0_" + name, directory=args.out)
+        else:
+            for i, ibo in enumerate(ibo_arr):
+                name = "ber_vs_ebn0_%s_ibo%d_ebn0_min%d_max%d_step%1.2f_niter%s" % (
+                    tag, ibo, min(ebn0_arr), max(ebn0_arr), ebn0_arr[1] - ebn0_arr[0],
+                    "_".join(str(v) for v in iters[1:]))
+                save_to_csv(ber_vs_ebn0_rows(ebn0_arr, ber[i].T), name, directory=args.out)
+        print(f"sweep done: {len(ibo_arr) * len(ebn0_arr)} points on {world} GPU(s) -> {args.out}")
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -104,23 +104,20 @@ def to_time_domain(in_sig_mat_fd: ndarray) -> ndarray:
 
 
 def save_to_csv(data_lst: list, filename: str, directory: str = "figs/csv_results") -> None:
-    """Row-per-array CSV, the reference's result layout (utilities.py:342-352, usage.rst:40-56)."""
+    """One row per vector, ``csv.writer.writerows`` (utilities.py:342-352); the reference
+    writes to ``figs/csv_results`` relative to the working directory."""
     import os
     os.makedirs(directory, exist_ok=True)
     with open(os.path.join(directory, "%s.csv" % filename), "w", newline="") as f:
-        w = csv.writer(f)
-        for row in data_lst:
-            w.writerow(list(np.asarray(row).reshape(-1)))
+        csv.writer(f).writerows([list(np.asarray(row, dtype=np.float64).reshape(-1)) for row in data_lst])
 
 
-def read_from_csv(filename: str, directory: str = "figs/csv_results") -> list:
-    """(utilities.py:355-365)"""
+def read_from_csv(filename: str, directory: str = "../figs/csv_results") -> list:
+    """List of float rows, ``QUOTE_NONNUMERIC`` (utilities.py:355-365; the reference reads
+    from ``../figs/csv_results``)."""
     import os
-    out = []
-    with open(os.path.join(directory, "%s.csv" % filename), newline="") as f:
-        for row in csv.reader(f):
-            out.append(np.asarray([float(v) for v in row]))
-    return out
+    with open(os.path.join(directory, "%s.csv" % filename), "r", newline="") as f:
+        return list(csv.reader(f, quoting=csv.QUOTE_NONNUMERIC))
 
 
 def print_progress_bar(iteration: int, total: int, prefix: str = "", suffix: str = "", decimals: int = 1,

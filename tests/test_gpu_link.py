@@ -60,3 +60,25 @@ def test_published_csv_point_rayleigh():
     sig = np.sqrt(pub / bits[0]) * 3
     print("paper-config BER", ber, "published", pub)
     assert np.all(np.abs(ber - pub) < 6 * sig + 0.03 * pub), (ber, pub)
+
+
+def test_sweep_grid_on_gpu_equals_per_point_runs():
+    """BASELINE config 4 machinery on one GPU: sweep.run_grid == independent per-point runs
+    (each point keyed by its grid index, so any sharding gives these numbers)."""
+    import sweep
+    from utilities import ebn0_to_snr
+    link, mod = build_link(n_ant=8, n_sc=256, n_fft=512, M=16, bits_sent_max=1024 * 64, n_err_min=500)
+    ibo, ebn0 = [0.0, 2.0], [6.0, 9.0, 12.0]
+    err, bits = sweep.run_grid(link, ibo, ebn0, [0, 1], True, seed=11)
+    link2, _ = build_link(n_ant=8, n_sc=256, n_fft=512, M=16, bits_sent_max=1024 * 64, n_err_min=500)
+    for i, b in enumerate(ibo):
+        link2.update_distortion(b)
+        for j, e in enumerate(ebn0):
+            link2.set_snr(float(ebn0_to_snr(e, 256, 256, 16)))
+            ee, bb = shared(3)
+            link2.simulate(True, True, np.array([0, 1]), sweep.point_seed(11, i * len(ebn0) + j), ee, bb)
+            np.testing.assert_array_equal(err[i, j], np.asarray(ee[:], np.int64))
+            np.testing.assert_array_equal(bits[i, j], np.asarray(bb[:], np.int64))
+    ber = sweep.ber_from_counts(err, bits)
+    assert np.all(np.diff(ber[:, :, 1], axis=1) <= 0)  # BER falls with Eb/N0
+    assert np.all(bits[..., 0] >= 1024 * 64) or np.all(err[..., 0] >= 500)

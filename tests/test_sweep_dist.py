@@ -1,0 +1,97 @@
+"""Grid sweep sharding + the single counter collective, on CPU with gloo (world_size 2),
+and the reference CSV layouts / fixed-BER interpolation."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as tmp
+
+
+class FakeModem:
+    n_sub_carr, constel_size = 64, 16
+
+
+class FakeLink:
+    """Deterministic Link stand-in: counters depend only on (ibo, snr, seed, index)."""
+    my_mod = FakeModem()
+
+    def __init__(self):
+        self.ibo = None
+        self.snr = None
+
+    def update_distortion(self, ibo_val_db):
+        self.ibo = ibo_val_db
+
+    def set_snr(self, snr_db_val):
+        self.snr = snr_db_val
+
+    def simulate(self, incl_clean, reroll, iters, seed_arr, err, bits):
+        n = len(iters) + (1 if incl_clean else 0)
+        for i in range(n):
+            bits[i] += 256 * 100
+            err[i] += int(1000 * np.exp(-0.2 * self.snr) * (1 + i) * (1 + self.ibo)) + seed_arr[1] % 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    import torch.distributed as dist
+    import sweep
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    err, bits = sweep.run_grid(FakeLink(), [0.0, 1.0, 2.0], np.arange(5.0, 15.0, 2.0), [0, 1, 2], True, 7, rank,
+                               world, dist)
+    np.save(os.path.join(out, f"r{rank}.npy"), np.stack([err, bits]))
+    dist.destroy_process_group()
+
+
+def test_sharded_sweep_matches_single_process(tmp_path):
+    import sweep
+    ref_err, ref_bits = sweep.run_grid(FakeLink(), [0.0, 1.0, 2.0], np.arange(5.0, 15.0, 2.0), [0, 1, 2], True, 7)
+    tmp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        got = np.load(os.path.join(tmp_path, f"r{r}.npy"))
+        np.testing.assert_array_equal(got[0], ref_err)
+        np.testing.assert_array_equal(got[1], ref_bits)
+    assert ref_err.shape == (3, 5, 4)
+
+
+def test_owned_points_partition():
+    import sweep
+    for world in (1, 2, 3, 8):
+        pts = sorted(p for r in range(world) for p in sweep.owned_points(37, r, world))
+        assert pts == list(range(37))
+
+
+def test_required_ebn0_and_csv_layout(tmp_path):
+    import sweep
+    import utilities
+    ebn0 = np.arange(10.0, 13.1, 1.0)
+    ber = np.zeros((2, 4, 2))
+    ber[:, :, 0] = [[0.1, 0.03, 0.005, 0.001], [0.2, 0.1, 0.05, 0.02]]
+    ber[:, :, 1] = [[0.05, 0.01, 0.002, 0.0005], [0.1, 0.05, 0.011, 0.003]]
+    req = sweep.required_ebn0(ber, ebn0, 1e-2)
+    assert req[0, 0] == pytest.approx(11 + (0.03 - 0.01) / (0.03 - 0.005), rel=1e-12)
+    assert req[0, 1] == np.inf  # target outside the measured range
+    assert req[1, 0] == pytest.approx(11.0)
+    rows = sweep.fixed_ber_rows([0.0, 0.5], ber)
+    assert len(rows) == 1 + 2 * 4 and list(rows[0]) == [0.0, 0.5]
+    utilities.save_to_csv(rows, "fixed", directory=str(tmp_path))
+    back = utilities.read_from_csv("fixed", directory=str(tmp_path))
+    np.testing.assert_allclose(back[1], ber[0, 0])
+    assert sweep.ber_from_counts([1, 0], [0, 4])[0] != sweep.ber_from_counts([1, 0], [0, 4])[0]  # NaN
+
+
+def test_published_csv_layout_readable():
+    """The reference's own CSV (ber_vs_ebn0 layout) parses with our reader."""
+    import utilities
+    d = os.path.join(os.path.dirname(__file__), "golden")
+    rows = utilities.read_from_csv("published_ber_vs_ebn0_cnc_rayleigh_ibo3", directory=d)
+    assert rows[0][0] == 5.0 and len(rows) == 11 and len(rows[1]) == 16
