@@ -88,7 +88,7 @@ def cpu_baseline(seconds=15.0):
 
 def load_pmc_traffic(trials_per_launch):
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if one matches."""
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "*pmc*.json"), recursive=True), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
