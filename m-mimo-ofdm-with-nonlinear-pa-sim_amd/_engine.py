@@ -127,7 +127,7 @@ class Engine:
         h = L.mimo_engine_create(ctypes.byref(cfg))
         if not h:
             raise ValueError(L.mimo_last_error().decode())
-        self._h = h
+        self._h, self._L = h, L   # the library this handle belongs to
         self.n_sub_carr, self.constel_size = n_sub_carr, constel_size
 
     def set_point(self, ibo_db, snr_db, avg_symbol_power, pa_kind, sat_pow=0.0, p_hardness=0.0, toi_coeff=0.0,
@@ -137,7 +137,7 @@ class Engine:
                        sat_pow=float(sat_pow), p_hardness=float(p_hardness), toi_coeff=float(toi_coeff),
                        cnc_sat_pow=float(cnc_sat_pow), cnc_toi_coeff=float(cnc_toi_coeff),
                        cnc_alpha=float(cnc_alpha), csi_eps=-1.0 if csi_eps is None else float(csi_eps))
-        _check(lib().mimo_engine_set_point(self._h, ctypes.byref(pt)))
+        _check(self._L.mimo_engine_set_point(self._h, ctypes.byref(pt)))
 
     def run(self, seed, first_trial, n_trials, iters, incl_clean=False, per_trial=False):
         """-> (err[n_idx], bits[n_idx], per_trial[n_trials, n_idx] or None)."""
@@ -146,7 +146,7 @@ class Engine:
         err = np.zeros(n_idx, np.uint64)
         bits = np.zeros(n_idx, np.uint64)
         pt = np.zeros((int(n_trials), n_idx), np.uint32) if per_trial else None
-        _check(lib().mimo_engine_run(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(first_trial), int(n_trials),
+        _check(self._L.mimo_engine_run(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(first_trial), int(n_trials),
                                      _ptr(it, ctypes.c_int32), len(it), int(bool(incl_clean)),
                                      _ptr(err, ctypes.c_uint64), _ptr(bits, ctypes.c_uint64),
                                      _ptr(pt, ctypes.c_uint32) if pt is not None else None))
@@ -154,14 +154,14 @@ class Engine:
 
     @property
     def kernel_ms(self):
-        return lib().mimo_engine_last_kernel_ms(self._h)
+        return self._L.mimo_engine_last_kernel_ms(self._h)
 
     def describe(self):
-        return lib().mimo_engine_describe(self._h).decode()
+        return self._L.mimo_engine_describe(self._h).decode()
 
     def close(self):
         if getattr(self, "_h", None):
-            lib().mimo_engine_destroy(self._h)
+            self._L.mimo_engine_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -23,9 +23,17 @@ struct Key {
   uint32_t k0, k1;
 };
 
+// a ^ b ^ k in one VALU op: gfx950 has no v_xor3_b32 but has v_bitop3_b32 (LUT 0x96).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t k) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+  return r;
+}
+
 // One round = 2 x v_mad_u64_u32 (the full 64-bit product in one ~4-cycle wave64
-// instruction) + 4 x v_xor_b32, instead of mul_hi + mul_lo per word: every 32-bit integer
-// op is half rate on gfx950 (tools/microbench/ops.hip); gfx950 has no v_xor3_b32.
+// instruction) + 2 x v_bitop3_b32, instead of mul_hi + mul_lo + 2 xor per word: every
+// 32-bit integer op is half rate on gfx950 (tools/microbench/ops.hip).  The key words are
+// uniform (SGPRs), the one scalar operand a VOP3 op may take.
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, Key key) {
   uint32_t k0 = key.k0, k1 = key.k1;
 #pragma unroll
@@ -36,7 +44,8 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, Key key) {
     }
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
-    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0);
+    c = make_uint4(xor3((uint32_t)(p1 >> 32), c.y, k0), (uint32_t)p1, xor3((uint32_t)(p0 >> 32), c.w, k1),
+                   (uint32_t)p0);
   }
   return c;
 }

@@ -47,6 +47,9 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
 __device__ __forceinline__ float2 cmulc(float2 a, float2 b) {  // a * conj(b)
   return make_float2(fmaf(a.x, b.x, a.y * b.y), fmaf(a.y, b.x, -a.x * b.y));
 }
+__device__ __forceinline__ float2 cmac(float2 acc, float2 a, float2 b) {  // acc + a * b, 4 FMAs
+  return make_float2(fmaf(a.x, b.x, fmaf(-a.y, b.y, acc.x)), fmaf(a.x, b.y, fmaf(a.y, b.x, acc.y)));
+}
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
 
 // x * exp(DIR * j * 2 pi * M / R) with the trivial angles resolved at compile time.
@@ -126,7 +129,7 @@ struct Dft {
 };
 
 // ---------------------------------------------------------------- team FFT
-template <int F, int T>
+template <int F, int T, int NBUF = 2>
 struct TeamFft {
   static constexpr int P = F / T;
   static constexpr int LOG_F = ilog2(F);
@@ -137,7 +140,14 @@ struct TeamFft {
 
   static constexpr int bits(int s) { return LOG_F / NST + (s < LOG_F % NST ? 1 : 0); }
   static constexpr int bits_before(int s) { return s == 0 ? 0 : bits_before(s - 1) + bits(s - 1); }
-  static __device__ __forceinline__ int pad(int e) { return e + (e >> 5); }
+  static __host__ __device__ constexpr int pad(int e) { return e + (e >> 5); }
+  // Global-address-space load (the laundered table pointer would otherwise be generic
+  // and compile to flat loads, which also count against lgkmcnt with the LDS traffic).
+  static __device__ __forceinline__ float2 gload(const float2* p, int i) {
+    typedef float v2f __attribute__((ext_vector_type(2)));
+    const v2f v = ((const __attribute__((address_space(1))) v2f*)p)[i];
+    return make_float2(v.x, v.y);
+  }
 
   // Exchange buffers alternate (stage S of a transform started at parity PAR uses buffer
   // (S + PAR) & 1), so a write never targets the buffer other threads may still be
@@ -153,7 +163,10 @@ struct TeamFft {
     constexpr int B = P / R;
     constexpr bool LAST = (S == NST - 1);
     static_assert(B >= 1 && B * R == P, "radix must divide points per thread");
-    float2* buf = lds + ((S + PAR) & 1) * LDS_ELEMS;
+    float2* buf = lds + (NBUF == 2 ? ((S + PAR) & 1) * LDS_ELEMS : 0);
+    if constexpr (NBUF == 1 && !LAST) {
+      if (!no_xchg) __syncthreads();  // everyone has read the previous exchange
+    }
 #pragma unroll
     for (int i = 0; i < B; ++i) {
       float2 v[R];
@@ -165,7 +178,7 @@ struct TeamFft {
         const int step = jm * (F / (NS * R));
 #pragma unroll
         for (int r = 1; r < R; ++r) {
-          const float2 w = tw[step * r];  // exp(-j 2 pi e / F)
+          const float2 w = gload(tw, step * r);  // exp(-j 2 pi e / F)
           v[r] = DIR < 0 ? cmul(v[r], w) : cmulc(v[r], w);
         }
       }
@@ -177,16 +190,19 @@ struct TeamFft {
 #pragma unroll
         for (int r = 0; r < R; ++r) d[i + r * B] = v[r];
       } else {
-        const int base = (j / NS) * NS * R + jm;
+        // pad(base + r NS) == pad(base) + pad(r NS) for power-of-two NS, R, T (the
+        // padding never splits a write group): one address per i, immediate offsets.
+        float2* wb = buf + pad((j / NS) * NS * R + jm);
 #pragma unroll
-        for (int r = 0; r < R; ++r) buf[pad(base + r * NS)] = v[r];
+        for (int r = 0; r < R; ++r) wb[pad(r * NS)] = v[r];
       }
     }
     if constexpr (!LAST) {
       if (!no_xchg) {
         __syncthreads();
+        const float2* rb = buf + pad(t);
 #pragma unroll
-        for (int m = 0; m < P; ++m) d[m] = buf[pad(t + T * m)];
+        for (int m = 0; m < P; ++m) d[m] = rb[pad(T * m)];
       }
     }
   }
@@ -201,7 +217,7 @@ struct TeamFft {
   }
 
   static constexpr int XCHG = NST - 1;  // exchanges per transform
-  static constexpr int LDS_TOTAL = 2 * LDS_ELEMS;  // two exchange buffers
+  static constexpr int LDS_TOTAL = NBUF * LDS_ELEMS;  // exchange buffer(s)
 
   // Un-normalised transform of the team's cyclic-distributed vector.  Ends with the
   // last exchange's reads done by this thread only: callers that touch `lds` next must

@@ -32,6 +32,9 @@ enum ChanKind : int { CH_RAYLEIGH = 1, CH_LOS = 2, CH_TWOPATH = 3 };
 enum RxKind : int { RX_CNC = 1, RX_MCNC = 2 };
 
 constexpr int kMaxWaves = 16;
+#ifndef MIMO_NBUF
+#define MIMO_NBUF 2
+#endif
 
 struct TrialParams {
   uint64_t seed;
@@ -175,6 +178,22 @@ __device__ __forceinline__ float2 pa_apply(int kind, float2 x, float sat, float 
   return make_float2(x.x * sc, x.y * sc);
 }
 
+// PA on all P samples of a thread: one uniform branch on the kind, then a straight loop.
+template <int P>
+__device__ __forceinline__ void pa_block(int kind, float2 (&d)[P], float sat, float sqrt_sat, float inv_sat,
+                                         float rapp_p, float toi) {
+  if (kind == PA_SOFTLIM) {
+#pragma unroll
+    for (int m = 0; m < P; ++m) d[m] = pa_apply(PA_SOFTLIM, d[m], sat, sqrt_sat, inv_sat, rapp_p, toi);
+  } else if (kind == PA_RAPP) {
+#pragma unroll
+    for (int m = 0; m < P; ++m) d[m] = pa_apply(PA_RAPP, d[m], sat, sqrt_sat, inv_sat, rapp_p, toi);
+  } else if (kind == PA_TOI) {
+#pragma unroll
+    for (int m = 0; m < P; ++m) d[m] = pa_apply(PA_TOI, d[m], sat, sqrt_sat, inv_sat, rapp_p, toi);
+  }
+}
+
 // Per-axis hard slicer == argmin |z - C| over the Gray-ordered constellation with the
 // reference's first-index (lowest label) tie-break (modulation.py:75-76,138-146).
 __device__ __forceinline__ uint32_t gray(uint32_t i) { return i ^ (i >> 1); }
@@ -248,7 +267,10 @@ struct Channel {
   }
 
   // True channel of antenna a at the thread's slots (relative scale: common factors
-  // cancel in MRT, AGC and the SNR normalisation).
+  // cancel in MRT, AGC and the SNR normalisation).  FREL = false leaves out the
+  // per-sub-carrier FSPL factor fc/f_k, which the kernel then applies once per trial
+  // (it cancels in the MRT precoder; see the kernel's AWGN step).
+  template <bool FREL>
   static __device__ __forceinline__ void gen(const TrialParams& p, Key key, uint32_t trial, int a, int t,
                                              const double (&rx)[3], float2 (&h)[NSLOT]) {
     const int S = p.n_sc;
@@ -265,7 +287,7 @@ struct Channel {
       for (int s = 0; s < NSLOT; ++s) {
         bool v;
         const int k = SL::k_of(s, t, S, v);
-        const float sc = v ? sa * p.f_rel[k] : 0.f;
+        const float sc = v ? (FREL ? sa * p.f_rel[k] : sa) : 0.f;
         h[s] = cscale(h[s], sc);
       }
     } else {
@@ -290,7 +312,7 @@ struct Channel {
         float2 hv = make_float2(0.f, 0.f);
         if (v) {
           const double foc = p.f_over_c[k];
-          const float fr = p.f_rel[k];
+          const float fr = FREL ? p.f_rel[k] : 1.0f;
           double ph = d_los * foc;
           ph -= floor(ph);
           const float a1 = att_los * fr;
@@ -311,12 +333,18 @@ struct Channel {
 
 // ---------------------------------------------------------------- the kernel
 template <int F, int T, int NSLOT, bool ALIGNED, int CH, bool CSI, int MINW>
-__global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
-  using FFT = TeamFft<F, T>;
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void trial_kernel(TrialParams p) {
+  using FFT = TeamFft<F, T, MIMO_NBUF>;
   using SL = Slots<F, T, NSLOT, ALIGNED>;
   using CHN = Channel<F, T, NSLOT, ALIGNED, CH>;
   constexpr int P = FFT::P;
   constexpr int W = T / 64;
+  // Without CSI errors the channel factors as H[a,k] = f_rel[k] H'[a,k]: f_rel cancels in
+  // the MRT precoder and in vk_pow, scales r and g by f_rel, and enters only through the
+  // AGC power eta and the noise term z = r'/g' + sigma n / (f_rel g').  The antenna loops
+  // then run on H' (no per-antenna table reads).  With CSI the estimate's error power
+  // mixes sub-carriers, so H keeps the factor.
+  constexpr bool FREL = CSI;
 
   __shared__ float2 lds[FFT::LDS_TOTAL];
   __shared__ float red[kMaxWaves];
@@ -352,6 +380,16 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
     valid_mask |= (v ? 1u : 0u) << s;
   }
 
+  auto frel_of = [&](int s) __attribute__((always_inline)) -> float {
+    if constexpr (FREL) {
+      return 1.0f;
+    } else {
+      bool v;
+      const int k = SL::k_of(s, t, S, v);
+      return v ? p.f_rel[k] : 1.0f;
+    }
+  };
+
   // ---- pass 1: MRT norms over the (estimated) channel
   float nrm2[NSLOT];
 #pragma unroll
@@ -359,7 +397,7 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
   for (int a = 0; a < (MIMO_ABL(p, ABL_PASS1) ? 1 : A); ++a) {
     const int tl = opaque(t);
     float2 h[NSLOT];
-    CHN::gen(p, key, trial, a, tl, rx, h);
+    CHN::template gen<FREL>(p, key, trial, a, tl, rx, h);
     if constexpr (CSI) {
       // mp_model.py:264-282: Hhat = sqrt(1-eps^2) H + eps sqrt(mean_k |H|^2) z
       float pw = 0.f;
@@ -383,7 +421,8 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
   for (int s = 0; s < NSLOT; ++s) {
     const bool v = (valid_mask >> s) & 1u;
     inv_nrm[s] = v ? __builtin_amdgcn_rsqf(nrm2[s]) : 0.f;
-    etac_p += v ? nrm2[s] : 0.f;
+    const float fr = frel_of(s);
+    etac_p += v ? nrm2[s] * (fr * fr) : 0.f;
   }
   if constexpr (CSI) __syncthreads();  // pw_csi visible
 
@@ -401,17 +440,20 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
   // ---- array pass: precode -> IFFT -> PA -> FFT -> combine, one antenna at a time.
   // MAIN: symbols = tx labels, combine with the true channel, accumulate g (alpha_a).
   // MCNC: symbols = detected labels, combine with the estimated channel (corrector.py:198-200).
-  auto array_pass = [&](const uint32_t (&sym_lab)[NSLOT], bool main_pass, float2 (&acc)[NSLOT])
+  // The symbols enter pre-weighted, symw = s / ||Hhat|| / sqrt(F) (0 on invalid slots).
+  auto weighted_symbols = [&](const uint32_t (&lab_in)[NSLOT], float2 (&symw)[NSLOT])
+                              __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < NSLOT; ++s) symw[s] = cscale(qam_point(lab_in[s], L, hb), inv_nrm[s] * inv_sqrt_f);
+  };
+  auto array_pass = [&](const float2 (&symw)[NSLOT], bool main_pass, float2 (&acc)[NSLOT])
                         __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) acc[s] = make_float2(0.f, 0.f);
     for (int a = 0; a < A; ++a) {
       const int tl = opaque(t);
-      uint32_t sl[NSLOT];
-#pragma unroll
-      for (int s = 0; s < NSLOT; ++s) sl[s] = opaque(sym_lab[s]);
       float2 h[NSLOT];
-      CHN::gen(p, key, trial, a, tl, rx, h);
+      CHN::template gen<FREL>(p, key, trial, a, tl, rx, h);
       float2 he[CSI ? NSLOT : 1];
       if constexpr (CSI) {
         float2 zc[NSLOT];
@@ -429,15 +471,9 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
         const float2 e = hest(s);
-        const float wgt = inv_nrm[s] * inv_sqrt_f;
-        const float2 sym = qam_point(sl[s], L, hb);
-        x[s] = cscale(cmulc(sym, e), wgt);  // s conj(Hhat) / ||Hhat|| / sqrt(F)
-        if ((valid_mask >> s) & 1u) {
-          const float e2 = fmaf(e.x, e.x, e.y * e.y);
-          vk = fmaf(e2, inv_nrm[s] * inv_nrm[s], vk);
-        } else {
-          x[s] = make_float2(0.f, 0.f);
-        }
+        x[s] = cmulc(symw[s], e);  // s conj(Hhat) / ||Hhat|| / sqrt(F); 0 off band (symw = 0)
+        const float e2 = fmaf(e.x, e.x, e.y * e.y);
+        vk = fmaf(e2, inv_nrm[s] * inv_nrm[s], vk);  // inv_nrm = 0 off band
       }
       if (main_pass) {
         vk = wave_sum(vk);
@@ -445,11 +481,7 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
       }
       SL::scatter(d, x, t0);
       if (!MIMO_ABL(p, ABL_FFT)) FFT::template run<+1>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG));
-      if (!MIMO_ABL(p, ABL_PA)) {
-#pragma unroll
-        for (int m = 0; m < P; ++m)
-          d[m] = pa_apply(p.pa_kind, d[m], p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
-      }
+      if (!MIMO_ABL(p, ABL_PA)) pa_block(p.pa_kind, d, p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
       if (!MIMO_ABL(p, ABL_FFT)) FFT::template run_second<-1>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG));
       if (MIMO_ABL(p, ABL_FFT)) __syncthreads();  // keep the vk_part hand-off ordered
       float alpha_a = 0.f;
@@ -463,12 +495,12 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
       for (int s = 0; s < NSLOT; ++s) {
         const float2 y = SL::gather(d, s, t0);
         if (main_pass) {
-          acc[s] = cadd(acc[s], cmul(h[s], y));
+          acc[s] = cmac(acc[s], h[s], y);
           const float2 e = hest(s);
           g[s] = fmaf(alpha_a * inv_nrm[s], fmaf(e.x, e.x, e.y * e.y), g[s]);
           if constexpr (CSI) cc[s] = cadd(cc[s], cscale(cmulc(h[s], e), inv_nrm[s]));
         } else {
-          acc[s] = cadd(acc[s], cmul(hest(s), y));
+          acc[s] = cmac(acc[s], hest(s), y);
         }
       }
     }
@@ -476,14 +508,21 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
     for (int s = 0; s < NSLOT; ++s) acc[s] = cscale(acc[s], inv_sqrt_f);
   };
 
-  array_pass(lab, true, r);
+  {
+    float2 symw[NSLOT];
+    weighted_symbols(lab, symw);
+    array_pass(symw, true, r);
+  }
 
   // ---- AWGN + AGC (noise.py:56-83 on all bins; only in-band bins matter)
   float2 zn[NSLOT];
   CHN::normals(key, trial, ST_NOISE, 0u, t, S, zn);
   float eta_p = 0.f;
 #pragma unroll
-  for (int s = 0; s < NSLOT; ++s) eta_p = ((valid_mask >> s) & 1u) ? fmaf(g[s], g[s], eta_p) : eta_p;
+  for (int s = 0; s < NSLOT; ++s) {
+    const float gs = g[s] * frel_of(s);
+    eta_p = ((valid_mask >> s) & 1u) ? fmaf(gs, gs, eta_p) : eta_p;
+  }
   const float eta = team_sum<T>(eta_p, red) / (float)S;
   uint32_t* out = p.counts + (size_t)blockIdx.x * p.n_idx;
 
@@ -502,8 +541,9 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
       const float2 sym = qam_point(lab[s], L, hb);
       float2 rc;
       if constexpr (CSI) rc = cmul(cc[s], sym); else rc = cscale(sym, inv_nrm[s] > 0.f ? 1.0f / inv_nrm[s] : 0.f);
-      const float ig = inv_nrm[s];  // 1 / ||Hhat||
-      const float2 zc = make_float2((rc.x + sig_c * zn[s].x) * ig, (rc.y + sig_c * zn[s].y) * ig);
+      const float ig = inv_nrm[s];  // 1 / ||Hhat||  (/ f_rel when factored)
+      const float sn = sig_c / frel_of(s);
+      const float2 zc = make_float2((rc.x + sn * zn[s].x) * ig, (rc.y + sn * zn[s].y) * ig);
       const uint32_t lh = slice(zc, L, hb);
       errs += ((valid_mask >> s) & 1u) ? __popc(lh ^ lab[s]) : 0u;
     }
@@ -515,7 +555,8 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
 #pragma unroll
   for (int s = 0; s < NSLOT; ++s) {
     const float ig = ((valid_mask >> s) & 1u) ? 1.0f / g[s] : 0.f;
-    z[s] = make_float2((r[s].x + sig * zn[s].x) * ig, (r[s].y + sig * zn[s].y) * ig);
+    const float sn = sig / frel_of(s);
+    z[s] = make_float2((r[s].x + sn * zn[s].x) * ig, (r[s].y + sn * zn[s].y) * ig);
   }
 
   // ---- CNC / MCNC receiver
@@ -541,9 +582,7 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
         x[s] = ((valid_mask >> s) & 1u) ? cscale(qam_point(lh[s], L, hb), inv_sqrt_f) : make_float2(0.f, 0.f);
       SL::scatter(d, x, t0);
       FFT::template run<+1>(d, lds, p.tw, t);
-#pragma unroll
-      for (int m = 0; m < P; ++m)
-        d[m] = pa_apply(p.cnc_pa_kind, d[m], p.sat_cnc, p.sqrt_sat_cnc, p.inv_sat_cnc, p.rapp_p, p.toi_cnc);
+      pa_block(p.cnc_pa_kind, d, p.sat_cnc, p.sqrt_sat_cnc, p.inv_sat_cnc, p.rapp_p, p.toi_cnc);
       FFT::template run_second<-1>(d, lds, p.tw, t);
       const float sc = inv_sqrt_f * p.inv_alpha_cnc;
 #pragma unroll
@@ -552,8 +591,9 @@ __global__ __launch_bounds__(T, MINW) void trial_kernel(TrialParams p) {
         dist[s] = ((valid_mask >> s) & 1u) ? csub(cscale(y, sc), qam_point(lh[s], L, hb)) : make_float2(0.f, 0.f);
       }
     } else {
-      float2 est[NSLOT];
-      array_pass(lh, false, est);
+      float2 est[NSLOT], symw[NSLOT];
+      weighted_symbols(lh, symw);
+      array_pass(symw, false, est);
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
         const float ig = ((valid_mask >> s) & 1u) ? 1.0f / g[s] : 0.f;
