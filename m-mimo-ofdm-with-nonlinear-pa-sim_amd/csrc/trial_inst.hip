@@ -12,50 +12,70 @@ namespace mimo {
 namespace {
 
 constexpr int kF = INST_F;
+#ifndef MIMO_MINW16
+#define MIMO_MINW16 3  // waves/SIMD target of the 16-point aligned instances (A/B knob)
+#endif
 
-template <int T, int NSLOT, bool AL, int CH, bool CSI, int MINW>
+// Occupancy profile per instance (see trial_kernel): waves/SIMD target, exchange buffers,
+// symbols in LDS.  Measured on MI355X (tools/ab_libs.py, profiles/r01/ab_*.json):
+//  - aligned, 16 points/thread, F <= 4096: 3 waves/SIMD needs <= 168 VGPRs and
+//    <= 160 KiB / (3 waves x 4 SIMD / waves per team) of LDS -> one exchange buffer and
+//    the weighted symbols in LDS (F = 2048: 25 KiB / team).  Two-path channels need
+//    too many registers for it (spills) and stay at 2.
+//  - aligned, 8 points/thread: 4 waves/SIMD fit in 128 VGPRs with two buffers.
+//  - generic (unaligned band), 16 slots/thread: symbols in LDS to limit spills.
+struct Profile {
+  int minw, nbuf;
+  bool symw_lds;
+};
+constexpr Profile profile_for(int T, bool aligned, int ch) {
+  const int P = kF / T;
+  if (!aligned) return Profile{2, kF >= 8192 ? 1 : 2, true};
+  if (ch == CH_TWOPATH) return Profile{2, 2, false};  // fp64 geometry per antenna: register-heavy
+  if (P < 16) return Profile{4, 2, false};
+  if (kF <= 4096) return Profile{MIMO_MINW16, MIMO_MINW16 == 3 ? 1 : 2, MIMO_MINW16 == 3};
+  return Profile{2, 2, false};
+}
+
+template <int T, int NSLOT, bool AL, int CH, bool CSI>
 hipError_t go(dim3 grid, hipStream_t st, const TrialParams& p) {
-  hipLaunchKernelGGL((trial_kernel<kF, T, NSLOT, AL, CH, CSI, MINW>), grid, dim3(T), 0, st, p);
+  constexpr Profile pr = profile_for(T, AL, CH);
+  hipLaunchKernelGGL((trial_kernel<kF, T, NSLOT, AL, CH, CSI, pr.minw, pr.nbuf, pr.symw_lds>), grid, dim3(T), 0, st, p);
   return hipGetLastError();
 }
 
-template <int T, int NSLOT, bool AL, int MINW>
+template <int T, int NSLOT, bool AL>
 hipError_t by_channel(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams& p, bool* found) {
   *found = true;
   switch (k.ch) {
     case CH_RAYLEIGH:
-      return k.csi ? go<T, NSLOT, AL, CH_RAYLEIGH, true, MINW>(grid, st, p)
-                   : go<T, NSLOT, AL, CH_RAYLEIGH, false, MINW>(grid, st, p);
+      return k.csi ? go<T, NSLOT, AL, CH_RAYLEIGH, true>(grid, st, p)
+                   : go<T, NSLOT, AL, CH_RAYLEIGH, false>(grid, st, p);
     case CH_LOS:
-      return k.csi ? go<T, NSLOT, AL, CH_LOS, true, MINW>(grid, st, p) : go<T, NSLOT, AL, CH_LOS, false, MINW>(grid, st, p);
+      return k.csi ? go<T, NSLOT, AL, CH_LOS, true>(grid, st, p) : go<T, NSLOT, AL, CH_LOS, false>(grid, st, p);
     case CH_TWOPATH:
-      return k.csi ? go<T, NSLOT, AL, CH_TWOPATH, true, MINW>(grid, st, p)
-                   : go<T, NSLOT, AL, CH_TWOPATH, false, MINW>(grid, st, p);
+      return k.csi ? go<T, NSLOT, AL, CH_TWOPATH, true>(grid, st, p)
+                   : go<T, NSLOT, AL, CH_TWOPATH, false>(grid, st, p);
     default:
       *found = false;
       return hipSuccess;
   }
 }
 
-// Occupancy target (waves per SIMD) by points per thread: 16 points fit 2 waves/SIMD,
-// 8 points fit 4 (measured with -Rpass-analysis=kernel-resource-usage, no spills).
-constexpr int minw_for(int P) { return P >= 16 ? 2 : 4; }
-
 template <int T>
 hipError_t by_team(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams& p, bool* found) {
   constexpr int P = kF / T;
-  constexpr int MW = minw_for(P);
   if (k.aligned) {
     if constexpr (8 < P) {
-      if (k.nslot == 8) return by_channel<T, 8, true, MW>(k, grid, st, p, found);
+      if (k.nslot == 8) return by_channel<T, 8, true>(k, grid, st, p, found);
     }
     if constexpr (4 < P) {
-      if (k.nslot == 4) return by_channel<T, 4, true, MW>(k, grid, st, p, found);
+      if (k.nslot == 4) return by_channel<T, 4, true>(k, grid, st, p, found);
     }
     return hipSuccess;
   }
   if (k.nslot != P) return hipSuccess;
-  return by_channel<T, P, false, 2>(k, grid, st, p, found);
+  return by_channel<T, P, false>(k, grid, st, p, found);
 }
 
 }  // namespace

@@ -32,9 +32,6 @@ enum ChanKind : int { CH_RAYLEIGH = 1, CH_LOS = 2, CH_TWOPATH = 3 };
 enum RxKind : int { RX_CNC = 1, RX_MCNC = 2 };
 
 constexpr int kMaxWaves = 16;
-#ifndef MIMO_NBUF
-#define MIMO_NBUF 2
-#endif
 
 struct TrialParams {
   uint64_t seed;
@@ -332,9 +329,13 @@ struct Channel {
 };
 
 // ---------------------------------------------------------------- the kernel
-template <int F, int T, int NSLOT, bool ALIGNED, int CH, bool CSI, int MINW>
+// Occupancy tuning per instance (trial_inst.hip): MINW = waves/SIMD the register
+// allocation targets, NBUF = FFT exchange buffers (2: one barrier per exchange, 1: half
+// the LDS), SYMW_LDS = keep the pre-weighted symbols in LDS (thread-private) instead of
+// registers.  F = 2048 runs (3, 1, true): 25 KiB LDS and <= 168 VGPRs per 128-thread team.
+template <int F, int T, int NSLOT, bool ALIGNED, int CH, bool CSI, int MINW, int NBUF, bool SYMW_LDS>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void trial_kernel(TrialParams p) {
-  using FFT = TeamFft<F, T, MIMO_NBUF>;
+  using FFT = TeamFft<F, T, NBUF>;
   using SL = Slots<F, T, NSLOT, ALIGNED>;
   using CHN = Channel<F, T, NSLOT, ALIGNED, CH>;
   constexpr int P = FFT::P;
@@ -350,6 +351,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   __shared__ float red[kMaxWaves];
   __shared__ float vk_part[2][kMaxWaves];
   __shared__ float pw_csi[CSI ? 1024 : 1];
+  __shared__ float2 symw_s[SYMW_LDS ? NSLOT * T : 1];  // [slot][thread]
 
   const int t = threadIdx.x;
   const bool t0 = (t == 0);
@@ -369,14 +371,21 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     rx[2] = p.rx_z;
   }
 
-  // ---- transmitted labels and validity
-  uint32_t lab[NSLOT];
+  // ---- transmitted labels and validity.  Labels are drawn twice (for the symbols before
+  // the array pass, for the error counts after it) instead of being held across it.
   uint32_t valid_mask = 0;
+  auto gen_labels = [&](int tt, uint32_t (&lab_out)[NSLOT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < NSLOT; ++s) {
+      bool v;
+      const int k = SL::k_of(s, tt, S, v);
+      lab_out[s] = v ? qam_label(key, k, trial, p.label_mask) : 0u;
+    }
+  };
 #pragma unroll
   for (int s = 0; s < NSLOT; ++s) {
     bool v;
-    const int k = SL::k_of(s, t, S, v);
-    lab[s] = v ? qam_label(key, k, trial, p.label_mask) : 0u;
+    SL::k_of(s, t, S, v);
     valid_mask |= (v ? 1u : 0u) << s;
   }
 
@@ -441,13 +450,18 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // MAIN: symbols = tx labels, combine with the true channel, accumulate g (alpha_a).
   // MCNC: symbols = detected labels, combine with the estimated channel (corrector.py:198-200).
   // The symbols enter pre-weighted, symw = s / ||Hhat|| / sqrt(F) (0 on invalid slots).
-  auto weighted_symbols = [&](const uint32_t (&lab_in)[NSLOT], float2 (&symw)[NSLOT])
-                              __attribute__((always_inline)) {
+  float2 symw_r[SYMW_LDS ? 1 : NSLOT];
+  auto set_symbols = [&](const uint32_t (&lab_in)[NSLOT]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int s = 0; s < NSLOT; ++s) symw[s] = cscale(qam_point(lab_in[s], L, hb), inv_nrm[s] * inv_sqrt_f);
+    for (int s = 0; s < NSLOT; ++s) {
+      const float2 v = cscale(qam_point(lab_in[s], L, hb), inv_nrm[s] * inv_sqrt_f);
+      if constexpr (SYMW_LDS) symw_s[s * T + t] = v; else symw_r[s] = v;
+    }
   };
-  auto array_pass = [&](const float2 (&symw)[NSLOT], bool main_pass, float2 (&acc)[NSLOT])
-                        __attribute__((always_inline)) {
+  auto symw = [&](int s) __attribute__((always_inline)) -> float2 {
+    if constexpr (SYMW_LDS) return symw_s[s * T + t]; else return symw_r[s];
+  };
+  auto array_pass = [&](bool main_pass, float2 (&acc)[NSLOT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) acc[s] = make_float2(0.f, 0.f);
     for (int a = 0; a < A; ++a) {
@@ -471,7 +485,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
         const float2 e = hest(s);
-        x[s] = cmulc(symw[s], e);  // s conj(Hhat) / ||Hhat|| / sqrt(F); 0 off band (symw = 0)
+        x[s] = cmulc(symw(s), e);  // s conj(Hhat) / ||Hhat|| / sqrt(F); 0 off band (symw = 0)
         const float e2 = fmaf(e.x, e.x, e.y * e.y);
         vk = fmaf(e2, inv_nrm[s] * inv_nrm[s], vk);  // inv_nrm = 0 off band
       }
@@ -509,10 +523,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   };
 
   {
-    float2 symw[NSLOT];
-    weighted_symbols(lab, symw);
-    array_pass(symw, true, r);
+    uint32_t lab0[NSLOT];
+    gen_labels(t, lab0);
+    set_symbols(lab0);
   }
+  array_pass(true, r);
+  uint32_t lab[NSLOT];
+  gen_labels(opaque(t), lab);
 
   // ---- AWGN + AGC (noise.py:56-83 on all bins; only in-band bins matter)
   float2 zn[NSLOT];
@@ -591,9 +608,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         dist[s] = ((valid_mask >> s) & 1u) ? csub(cscale(y, sc), qam_point(lh[s], L, hb)) : make_float2(0.f, 0.f);
       }
     } else {
-      float2 est[NSLOT], symw[NSLOT];
-      weighted_symbols(lh, symw);
-      array_pass(symw, false, est);
+      float2 est[NSLOT];
+      set_symbols(lh);
+      array_pass(false, est);
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
         const float ig = ((valid_mask >> s) & 1u) ? 1.0f / g[s] : 0.f;

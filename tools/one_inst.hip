@@ -12,7 +12,7 @@
 #define XNS 8
 #endif
 #ifndef XMW
-#define XMW 2
+#define XMW 3
 #endif
 #ifndef XCH
 #define XCH 1
@@ -20,4 +20,7 @@
 #ifndef XCSI
 #define XCSI false
 #endif
-template __global__ void mimo::trial_kernel<XF, XT, XNS, true, XCH, XCSI, XMW>(mimo::TrialParams);
+#ifndef XNB
+#define XNB 1
+#endif
+template __global__ void mimo::trial_kernel<XF, XT, XNS, true, XCH, XCSI, XMW, XNB, XNB == 1>(mimo::TrialParams);
