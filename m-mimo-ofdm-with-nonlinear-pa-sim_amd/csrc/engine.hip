@@ -65,7 +65,7 @@ struct mimo_engine {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  float2* d_tw = nullptr;
+  float2* d_tw[2] = {nullptr, nullptr};  // stage twiddles for team_size(F), alt_team_size(F)
   float* d_ant_rel = nullptr;
   float* d_f_rel = nullptr;
   double* d_f_over_c = nullptr;
@@ -143,11 +143,23 @@ int ensure_device(mimo_engine* e) {
   HIP_TRY(hipEventCreate(&e->ev0));
   HIP_TRY(hipEventCreate(&e->ev1));
   const int F = e->cfg.n_fft, S = e->cfg.n_sub_carr, A = e->cfg.n_ant;
-  // twiddles exp(-j 2 pi e / F), computed in double
-  std::vector<float2> tw(F);
-  for (int i = 0; i < F; ++i) {
-    const double ang = -2.0 * M_PI * (double)i / (double)F;
-    tw[i] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+  // team-FFT stage twiddles per team size (team_fft.h plan), computed in double:
+  // stage s, entry [r][jm] = exp(-j 2 pi e / F) with e = jm r F / (NS R)
+  std::vector<float2> tws[2];
+  const int teams[2] = {mimo::team_size(F), mimo::alt_team_size(F)};
+  for (int v = 0; v < 2; ++v) {
+    const int P = F / teams[v];
+    tws[v].assign(std::max(1, mimo::fft_tw_total(F, P)), make_float2(0.f, 0.f));
+    for (int st = 1; st < mimo::fft_nst(F, P); ++st) {
+      const int NS = 1 << mimo::fft_bits_before(F, P, st), R = 1 << mimo::fft_bits(F, P, st);
+      float2* blk = tws[v].data() + mimo::fft_tw_off(F, P, st);
+      for (int r = 0; r < R; ++r)
+        for (int jm = 0; jm < NS; ++jm) {
+          const long e_idx = (long)jm * r * (F / (NS * R));
+          const double ang = -2.0 * M_PI * (double)e_idx / (double)F;
+          blk[r * NS + jm] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+        }
+    }
   }
   // in-band sub-carrier k -> bin (modulation.py:266-267)
   std::vector<float> f_rel(S);
@@ -172,13 +184,15 @@ int ensure_device(mimo_engine* e) {
   std::vector<float> ant_rel(A);
   for (int a = 0; a < A; ++a) ant_rel[a] = (float)(e->d0 / dist[a]);
 
-  HIP_TRY(hipMalloc(&e->d_tw, sizeof(float2) * F));
+  for (int v = 0; v < 2; ++v) {
+    HIP_TRY(hipMalloc(&e->d_tw[v], sizeof(float2) * tws[v].size()));
+    HIP_TRY(hipMemcpy(e->d_tw[v], tws[v].data(), sizeof(float2) * tws[v].size(), hipMemcpyHostToDevice));
+  }
   HIP_TRY(hipMalloc(&e->d_f_rel, sizeof(float) * S));
   HIP_TRY(hipMalloc(&e->d_f_over_c, sizeof(double) * S));
   HIP_TRY(hipMalloc(&e->d_ant_rel, sizeof(float) * A));
   HIP_TRY(hipMalloc(&e->d_tx_pos, sizeof(double) * 3 * A));
   HIP_TRY(hipMalloc(&e->d_tot, sizeof(unsigned long long) * 64));
-  HIP_TRY(hipMemcpy(e->d_tw, tw.data(), sizeof(float2) * F, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_f_rel, f_rel.data(), sizeof(float) * S, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_f_over_c, f_over_c.data(), sizeof(double) * S, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_ant_rel, ant_rel.data(), sizeof(float) * A, hipMemcpyHostToDevice));
@@ -258,7 +272,7 @@ int32_t mimo_engine_run(mimo_engine* e, uint64_t seed, uint64_t first_trial, uin
 
   mimo::TrialParams p{};
   p.seed = seed;
-  p.tw = e->d_tw;
+  p.tw = e->d_tw[key.T == mimo::team_size(c.n_fft) ? 0 : 1];
   p.ant_rel = e->d_ant_rel;
   p.f_rel = e->d_f_rel;
   p.f_over_c = e->d_f_over_c;
@@ -368,7 +382,8 @@ void mimo_engine_destroy(mimo_engine* e) {
   if (!e) return;
   if (e->ready) {
     (void)hipStreamSynchronize(e->stream);
-    (void)hipFree(e->d_tw);
+    (void)hipFree(e->d_tw[0]);
+    (void)hipFree(e->d_tw[1]);
     (void)hipFree(e->d_f_rel);
     (void)hipFree(e->d_f_over_c);
     (void)hipFree(e->d_ant_rel);

@@ -56,9 +56,11 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, Key key) {
 __device__ __forceinline__ float2 box_muller(uint32_t w0, uint32_t w1) {
   const float u1 = fmaf((float)w0, 2.3283064365386963e-10f, 1.1641532182693481e-10f);
   const float u2 = (float)w1 * 2.3283064365386963e-10f;
-  const float rho = __builtin_sqrtf(-0.69314718055994531f * __builtin_amdgcn_logf(u1));
-  const float rev = u2 >= 1.0f ? 0.0f : u2;  // (float)w1 may round up to 2^32
-  return make_float2(rho * __builtin_amdgcn_cosf(rev), rho * __builtin_amdgcn_sinf(rev));
+  // Raw v_sqrt_f32 (1 ulp): __builtin_sqrtf expands to ~15 instructions of IEEE
+  // correction.  u2 may round up to 1.0 (w1 > 2^32 - 128), which v_sin/v_cos treat as
+  // one full revolution, i.e. as 0.
+  const float rho = __builtin_amdgcn_sqrtf(-0.69314718055994531f * __builtin_amdgcn_logf(u1));
+  return make_float2(rho * __builtin_amdgcn_cosf(u2), rho * __builtin_amdgcn_sinf(u2));
 }
 
 __device__ __forceinline__ void cn_pair(Key key, uint32_t q, uint32_t trial, uint32_t stream, uint32_t aux,

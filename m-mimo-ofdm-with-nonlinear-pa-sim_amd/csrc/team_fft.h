@@ -39,6 +39,21 @@ constexpr double ct_sin(double x) { return ct_cos(x - kPi / 2); }
 
 constexpr int ilog2(int n) { return n <= 1 ? 0 : 1 + ilog2(n >> 1); }
 
+// ---------------------------------------------------------------- stage plan (host + device)
+// F points, P per thread: NST Stockham stages; stage s has radix 2^bits(s) and
+// NS = 2^bits_before(s).  Stage s >= 1 multiplies by twiddles exp(-j 2 pi jm r / (NS R)),
+// jm < NS, 1 <= r < R, stored per stage as a [R][NS] block (lane-contiguous in jm) of
+// one table; fft_tw_off(s) is the block's offset.
+constexpr int fft_nst(int F, int P) { return (ilog2(F) + ilog2(P) - 1) / ilog2(P); }
+constexpr int fft_bits(int F, int P, int s) {
+  return ilog2(F) / fft_nst(F, P) + (s < ilog2(F) % fft_nst(F, P) ? 1 : 0);
+}
+constexpr int fft_bits_before(int F, int P, int s) { return s == 0 ? 0 : fft_bits_before(F, P, s - 1) + fft_bits(F, P, s - 1); }
+constexpr int fft_tw_off(int F, int P, int s) {
+  return s <= 1 ? 0 : fft_tw_off(F, P, s - 1) + (1 << (fft_bits_before(F, P, s - 1) + fft_bits(F, P, s - 1)));
+}
+constexpr int fft_tw_total(int F, int P) { return fft_tw_off(F, P, fft_nst(F, P)); }
+
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
@@ -134,12 +149,12 @@ struct TeamFft {
   static constexpr int P = F / T;
   static constexpr int LOG_F = ilog2(F);
   static constexpr int LOG_P = ilog2(P);
-  static constexpr int NST = (LOG_F + LOG_P - 1) / LOG_P;
+  static constexpr int NST = fft_nst(F, P);
   static constexpr int LDS_ELEMS = F + F / 32;
   static_assert((1 << LOG_F) == F && (1 << LOG_P) == P && P >= 2, "power-of-two sizes");
 
-  static constexpr int bits(int s) { return LOG_F / NST + (s < LOG_F % NST ? 1 : 0); }
-  static constexpr int bits_before(int s) { return s == 0 ? 0 : bits_before(s - 1) + bits(s - 1); }
+  static constexpr int bits(int s) { return fft_bits(F, P, s); }
+  static constexpr int bits_before(int s) { return fft_bits_before(F, P, s); }
   static __host__ __device__ constexpr int pad(int e) { return e + (e >> 5); }
   // Global-address-space load (the laundered table pointer would otherwise be generic
   // and compile to flat loads, which also count against lgkmcnt with the LDS traffic).
@@ -175,10 +190,11 @@ struct TeamFft {
       const int j = t + T * i;
       const int jm = j & (NS - 1);
       if constexpr (NS > 1) {
-        const int step = jm * (F / (NS * R));
+        // [R][NS] block: uniform base per r (SGPRs) + the lane's jm as the VGPR offset
+        const float2* tws = tw + fft_tw_off(F, P, S);
 #pragma unroll
         for (int r = 1; r < R; ++r) {
-          const float2 w = gload(tw, step * r);  // exp(-j 2 pi e / F)
+          const float2 w = gload(tws + r * NS, jm);  // exp(-j 2 pi jm r / (NS R))
           v[r] = DIR < 0 ? cmul(v[r], w) : cmulc(v[r], w);
         }
       }

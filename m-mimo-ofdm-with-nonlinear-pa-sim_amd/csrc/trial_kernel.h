@@ -37,7 +37,7 @@ struct TrialParams {
   uint64_t seed;
   uint64_t first_trial;
   uint32_t* counts;              // [n_trials][n_idx]
-  const float2* tw;              // [F] exp(-j 2 pi e / F)
+  const float2* tw;              // team-FFT stage twiddles of (F, T) (team_fft.h fft_tw_off)
   const float* ant_rel;          // [A]  d0 / d_a      (Rayleigh FSPL, relative)
   const float* f_rel;            // [S]  fc / f_k      (f_k float32-quantised as in the reference)
   const double* f_over_c;        // [S]  f_k / c       (LoS / two-path phases)
@@ -228,22 +228,23 @@ struct Channel {
   static __device__ __forceinline__ void normals(Key key, uint32_t trial, uint32_t stream, uint32_t aux, int t, int S,
                                                  float2 (&z)[NSLOT]) {
     if constexpr (ALIGNED) {
+      // Pair indices in closed form (pair_of() applied to the aligned slot map):
+      //   positive band, slots j and j + Q: q = S/4 - 1 + t + T j, except thread 0 /
+      //   j = 0 (bins S/2 and S/4): q = S/2 - 1 with the two draws swapped;
+      //   negative band, slots HALF + j and HALF + j + Q: q = t + T j.
       constexpr int Q = SL::HALF / 2;
+      const bool t0 = (t == 0);
+      const int qp = (S >> 2) - 1 + t;
 #pragma unroll
-      for (int band = 0; band < 2; ++band) {
-#pragma unroll
-        for (int j = 0; j < Q; ++j) {
-          const int sa = band * SL::HALF + j, sb = sa + Q;
-          bool v;
-          const int k = SL::k_of(sa, t, S, v);
-          uint32_t q;
-          int slot;
-          pair_of(k, S, q, slot);
-          float2 z1, z2;
-          cn_pair(key, q, trial, stream, aux, z1, z2);
-          z[sa] = slot == 0 ? z1 : z2;
-          z[sb] = slot == 0 ? z2 : z1;
-        }
+      for (int j = 0; j < Q; ++j) {
+        float2 z1, z2;
+        const bool sw = (j == 0) && t0;
+        cn_pair(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, stream, aux, z1, z2);
+        z[j] = sw ? z2 : z1;
+        z[j + Q] = sw ? z1 : z2;
+        cn_pair(key, (uint32_t)(t + T * j), trial, stream, aux, z1, z2);
+        z[SL::HALF + j] = z1;
+        z[SL::HALF + j + Q] = z2;
       }
     } else {
 #pragma unroll

@@ -1,16 +1,16 @@
 # PMC passes for the fused trial kernel (one counter group per rocprofv3 run).
+# usage: bash tools/gpu_pmc.sh <outdir>
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc
+OUT=${1:-gpurun_out/pmc}
 mkdir -p $OUT
-BENCH="bench.py --no-cpu-baseline --steps 2 --warmup 1 --batch 16384"
-rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
+BENCH="bench.py --no-cpu-baseline --steps 2 --warmup 1"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" \
            "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT" \
            "SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 $BENCH > $OUT/p$i.log 2>&1 || echo "pass $i failed" >> $OUT/failed.txt
+  timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 $BENCH > $OUT/p$i.log 2>&1 || { echo "pass $i failed" >> $OUT/failed.txt; exit 1; }
 done
 echo done > $OUT/done.txt
