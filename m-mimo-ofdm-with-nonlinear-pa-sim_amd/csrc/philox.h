@@ -53,21 +53,23 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, Key key) {
 // Box-Muller on two words -> CN(0,1):  sqrt(-ln u1) * exp(j 2 pi u2),
 // u1 = (w0 + 0.5) 2^-32, u2 = w1 2^-32.  v_sin/v_cos take revolutions, so 2*pi*u2 is
 // never formed; v_log is log2.
-__device__ __forceinline__ float2 box_muller(uint32_t w0, uint32_t w1) {
+// c = -ln(2) scale^2 returns scale * CN(0,1) at no extra cost (v_log is log2).
+constexpr float kNegLn2 = -0.69314718055994531f;
+__device__ __forceinline__ float2 box_muller(uint32_t w0, uint32_t w1, float c = kNegLn2) {
   const float u1 = fmaf((float)w0, 2.3283064365386963e-10f, 1.1641532182693481e-10f);
   const float u2 = (float)w1 * 2.3283064365386963e-10f;
   // Raw v_sqrt_f32 (1 ulp): __builtin_sqrtf expands to ~15 instructions of IEEE
   // correction.  u2 may round up to 1.0 (w1 > 2^32 - 128), which v_sin/v_cos treat as
   // one full revolution, i.e. as 0.
-  const float rho = __builtin_amdgcn_sqrtf(-0.69314718055994531f * __builtin_amdgcn_logf(u1));
+  const float rho = __builtin_amdgcn_sqrtf(c * __builtin_amdgcn_logf(u1));
   return make_float2(rho * __builtin_amdgcn_cosf(u2), rho * __builtin_amdgcn_sinf(u2));
 }
 
 __device__ __forceinline__ void cn_pair(Key key, uint32_t q, uint32_t trial, uint32_t stream, uint32_t aux,
-                                        float2& z1, float2& z2) {
+                                        float2& z1, float2& z2, float c = kNegLn2) {
   const uint4 w = philox4x32_10(make_uint4(q, trial, stream, aux), key);
-  z1 = box_muller(w.x, w.y);
-  z2 = box_muller(w.z, w.w);
+  z1 = box_muller(w.x, w.y, c);
+  z2 = box_muller(w.z, w.w, c);
 }
 
 // Quarter pairing: sub-carrier k -> pair index q and slot (0: k1, 1: k2 = k1 + S/4).

@@ -163,7 +163,7 @@ __device__ __forceinline__ float2 pa_apply(int kind, float2 x, float sat, float 
   const float pw = fmaf(x.x, x.x, x.y * x.y);
   float sc = 1.0f;
   if (kind == PA_SOFTLIM) {
-    sc = pw > sat ? sqrt_sat * __builtin_amdgcn_rsqf(pw) : 1.0f;
+    sc = fminf(1.0f, sqrt_sat * __builtin_amdgcn_rsqf(pw));  // rsq(0) = inf -> 1
   } else if (kind == PA_RAPP) {
     // 1 / (1 + (pw/sat)^p)^(1/(2p))
     const float u = pw * inv_sat;
@@ -225,8 +225,9 @@ struct Channel {
   using SL = Slots<F, T, NSLOT, ALIGNED>;
 
   // CN(0,1) draws of one stream for the thread's slots (pairs resolved in-thread when aligned).
+  // c = -ln(2) scale^2 scales the draws (box_muller).
   static __device__ __forceinline__ void normals(Key key, uint32_t trial, uint32_t stream, uint32_t aux, int t, int S,
-                                                 float2 (&z)[NSLOT]) {
+                                                 float2 (&z)[NSLOT], float c = kNegLn2) {
     if constexpr (ALIGNED) {
       // Pair indices in closed form (pair_of() applied to the aligned slot map):
       //   positive band, slots j and j + Q: q = S/4 - 1 + t + T j, except thread 0 /
@@ -239,10 +240,10 @@ struct Channel {
       for (int j = 0; j < Q; ++j) {
         float2 z1, z2;
         const bool sw = (j == 0) && t0;
-        cn_pair(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, stream, aux, z1, z2);
+        cn_pair(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, stream, aux, z1, z2, c);
         z[j] = sw ? z2 : z1;
         z[j + Q] = sw ? z1 : z2;
-        cn_pair(key, (uint32_t)(t + T * j), trial, stream, aux, z1, z2);
+        cn_pair(key, (uint32_t)(t + T * j), trial, stream, aux, z1, z2, c);
         z[SL::HALF + j] = z1;
         z[SL::HALF + j + Q] = z2;
       }
@@ -257,7 +258,7 @@ struct Channel {
           int slot;
           pair_of(k, S, q, slot);
           float2 z1, z2;
-          cn_pair(key, q, trial, stream, aux, z1, z2);
+          cn_pair(key, q, trial, stream, aux, z1, z2, c);
           z[s] = slot == 0 ? z1 : z2;
         }
       }
@@ -273,20 +274,21 @@ struct Channel {
                                              const double (&rx)[3], float2 (&h)[NSLOT]) {
     const int S = p.n_sc;
     if constexpr (CH == CH_RAYLEIGH) {
+      const float sa = p.ant_rel[a];
       if (MIMO_ABL(p, ABL_RNG)) {
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s)
-          h[s] = make_float2(1.0f + 1e-3f * (float)((a + s + t) & 7), 0.5f - 1e-3f * (float)((a * s) & 3));
+          h[s] = make_float2(sa + 1e-3f * (float)((a + s + t) & 7), 0.5f - 1e-3f * (float)((a * s) & 3));
       } else {
-        normals(key, trial, ST_CHAN, (uint32_t)a, t, S, h);
+        normals(key, trial, ST_CHAN, (uint32_t)a, t, S, h, kNegLn2 * (sa * sa));  // ant_rel folded in
       }
-      const float sa = p.ant_rel[a];
+      if constexpr (FREL) {
 #pragma unroll
-      for (int s = 0; s < NSLOT; ++s) {
-        bool v;
-        const int k = SL::k_of(s, t, S, v);
-        const float sc = v ? (FREL ? sa * p.f_rel[k] : sa) : 0.f;
-        h[s] = cscale(h[s], sc);
+        for (int s = 0; s < NSLOT; ++s) {
+          bool v;
+          const int k = SL::k_of(s, t, S, v);
+          h[s] = cscale(h[s], v ? p.f_rel[k] : 0.f);
+        }
       }
     } else {
       const double tx = p.tx_pos[3 * a], ty = p.tx_pos[3 * a + 1], tz = p.tx_pos[3 * a + 2];
@@ -482,13 +484,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         if constexpr (CSI) return he[s]; else return h[s];
       };
       float2 x[NSLOT];
+      float e2[NSLOT];  // |Hhat|^2, kept for g after the FFT
       float vk = 0.f;
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
         const float2 e = hest(s);
         x[s] = cmulc(symw(s), e);  // s conj(Hhat) / ||Hhat|| / sqrt(F); 0 off band (symw = 0)
-        const float e2 = fmaf(e.x, e.x, e.y * e.y);
-        vk = fmaf(e2, inv_nrm[s] * inv_nrm[s], vk);  // inv_nrm = 0 off band
+        e2[s] = fmaf(e.x, e.x, e.y * e.y);
+        vk = fmaf(e2[s], inv_nrm[s] * inv_nrm[s], vk);  // inv_nrm = 0 off band
       }
       if (main_pass) {
         vk = wave_sum(vk);
@@ -511,8 +514,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         const float2 y = SL::gather(d, s, t0);
         if (main_pass) {
           acc[s] = cmac(acc[s], h[s], y);
+          g[s] = fmaf(alpha_a, e2[s], g[s]);  // sum_a alpha_a |Hhat|^2; x 1/||Hhat|| after the pass
           const float2 e = hest(s);
-          g[s] = fmaf(alpha_a * inv_nrm[s], fmaf(e.x, e.x, e.y * e.y), g[s]);
           if constexpr (CSI) cc[s] = cadd(cc[s], cscale(cmulc(h[s], e), inv_nrm[s]));
         } else {
           acc[s] = cmac(acc[s], hest(s), y);
@@ -529,6 +532,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     set_symbols(lab0);
   }
   array_pass(true, r);
+#pragma unroll
+  for (int s = 0; s < NSLOT; ++s) g[s] *= inv_nrm[s];
   uint32_t lab[NSLOT];
   gen_labels(opaque(t), lab);
 
