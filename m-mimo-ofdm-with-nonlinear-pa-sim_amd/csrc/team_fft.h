@@ -179,9 +179,6 @@ struct TeamFft {
     constexpr bool LAST = (S == NST - 1);
     static_assert(B >= 1 && B * R == P, "radix must divide points per thread");
     float2* buf = lds + (NBUF == 2 ? ((S + PAR) & 1) * LDS_ELEMS : 0);
-    if constexpr (NBUF == 1 && !LAST) {
-      if (!no_xchg) __syncthreads();  // everyone has read the previous exchange
-    }
 #pragma unroll
     for (int i = 0; i < B; ++i) {
       float2 v[R];
@@ -206,6 +203,12 @@ struct TeamFft {
 #pragma unroll
         for (int r = 0; r < R; ++r) d[i + r * B] = v[r];
       } else {
+        // One buffer: everyone must have read the previous exchange before it is
+        // overwritten.  The barrier sits after this stage's twiddle loads and DFT, so
+        // their latency overlaps the previous exchange's reads.
+        if constexpr (NBUF == 1) {
+          if (i == 0) __syncthreads();
+        }
         // pad(base + r NS) == pad(base) + pad(r NS) for power-of-two NS, R, T (the
         // padding never splits a write group): one address per i, immediate offsets.
         float2* wb = buf + pad((j / NS) * NS * R + jm);
