@@ -179,7 +179,7 @@ def main():
             "achieved": round(f_alg / avg_kernel_s / 1e12, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(f_alg / avg_kernel_s / 1e12 / FP32_PEAK_TFLOPS, 4),
             "traffic": traffic, "traffic_source": traffic_src,
-            "kernel": "mimo::trial_kernel<2048,128,8,aligned,rayleigh>", "kernel_ms": round(avg_kernel_s * 1e3, 3),
+            "kernel": "mimo::trial_kernel<2048,128,8,aligned,rayleigh,no-csi,3 waves/SIMD,1 buffer,symbols in LDS>", "kernel_ms": round(avg_kernel_s * 1e3, 3),
             "flops_alg_per_trial": flops_alg_per_trial(),
         },
         "hbm_alg": {"achieved": round(b_alg / avg_kernel_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
