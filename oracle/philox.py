@@ -93,11 +93,11 @@ def _check_sc(n_sc):
         raise ValueError("the engine requires n_sub_carr % 4 == 0 (sub-carrier pairing)")
 
 
-def qam_labels(seed, trials, n_sc, constel_size):
-    """[T, S] int64 QAM labels (stream BITS)."""
+def qam_labels(seed, trials, n_sc, constel_size, user=0):
+    """[T, S] int64 QAM labels (stream BITS; aux = user index for multi-user runs)."""
     trials = np.asarray(trials, dtype=np.uint64).reshape(-1, 1)
     k = np.arange(n_sc, dtype=np.uint64).reshape(1, -1)
-    w = philox4x32_10(k >> np.uint64(2), trials, STREAM_BITS, 0, seed)
+    w = philox4x32_10(k >> np.uint64(2), trials, STREAM_BITS, int(user), seed)
     sel = (k & np.uint64(3)).astype(np.int64)
     words = np.stack(w, axis=-1)  # [T, S, 4]
     word = np.take_along_axis(words, np.broadcast_to(sel, words.shape[:2])[..., None], axis=-1)[..., 0]
