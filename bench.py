@@ -27,6 +27,21 @@ for _p in (REPO, PKG):
 
 import numpy as np  # noqa: E402
 
+# Workloads: "2" is BASELINE configs[1] (the headline, default); the others are optional
+# extra lines: "paper" = the published CSV config (64 ant, FFT 4096, 2048 sc), "5su" =
+# BASELINE config 5's array / FFT / PA (256 ant, FFT 8192, 4096 sc, Rapp p=3) at one
+# user (the multi-user precoder is not built).
+WORKLOADS = {
+    "2": dict(A=64, S=1024, F=2048, M=64, CP=128, pa="softlim", p=0.0, ibo=3.0, ebn0=15.0,
+              desc="BASELINE config 2: 64-ant MRT, 1024-sc (FFT 2048) 64-QAM, soft limiter IBO 3 dB, "
+                   "Rayleigh, Eb/N0 15 dB"),
+    "paper": dict(A=64, S=2048, F=4096, M=64, CP=128, pa="softlim", p=0.0, ibo=3.0, ebn0=15.0,
+                  desc="paper config: 64-ant MRT, 2048-sc (FFT 4096) 64-QAM, soft limiter IBO 3 dB, Rayleigh, "
+                       "Eb/N0 15 dB"),
+    "5su": dict(A=256, S=4096, F=8192, M=64, CP=128, pa="rapp", p=3.0, ibo=3.0, ebn0=15.0,
+                desc="config-5 array at one user: 256-ant MRT, 4096-sc (FFT 8192) 64-QAM, Rapp p=3 IBO 3 dB, "
+                     "Rayleigh, Eb/N0 15 dB"),
+}
 A, S, F, M, CP = 64, 1024, 2048, 64, 128
 IBO, EBN0 = 3.0, 15.0
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -43,7 +58,7 @@ def flops_alg_per_trial(a=A, s=S, f=F):
     return a * (10 * f * np.log2(f) + 14 * s + 12 * f)
 
 
-def make_engine(device):
+def make_engine(device, workload="2"):
     import _engine
     import mp_model  # noqa: F401  (host mirror; computes the per-point scalars like Link)
     from utilities import ebn0_to_snr
@@ -53,8 +68,12 @@ def make_engine(device):
     from distortion import SoftLimiter
     import channel, noise, copy
 
+    w = WORKLOADS[workload]
+    A, S, F, M, CP = w["A"], w["S"], w["F"], w["M"], w["CP"]
+    from distortion import Rapp
     mod = OfdmQamModem(constel_size=M, n_fft=F, n_sub_carr=S, cp_len=CP)
-    dist = SoftLimiter(0, mod.avg_sample_power)
+    dist = SoftLimiter(0, mod.avg_sample_power) if w["pa"] == "softlim" else \
+        Rapp(0, mod.avg_sample_power, p_hardness=w["p"])
     tx = Transceiver(modem=copy.deepcopy(mod), impairment=copy.deepcopy(dist), center_freq=int(3.5e9),
                      carrier_spacing=int(15e3))
     rx = Transceiver(modem=copy.deepcopy(mod), impairment=copy.deepcopy(dist), cord_x=212, cord_y=212, cord_z=1.5,
@@ -64,25 +83,28 @@ def make_engine(device):
     ch = channel.MisoRayleighFd(tx_transceivers=arr.array_elements, rx_transceiver=rx, seed=1234)
     link = mp_model.Link(mod_obj=mod, array_obj=arr, std_rx_obj=rx, chan_obj=ch, noise_obj=noise.Awgn(snr_db=10),
                          rx_loc_var=10.0, n_err_min=10 ** 12, bits_sent_max=10 ** 15, is_mcnc=False, device=device)
-    link.update_distortion(ibo_val_db=IBO)
-    link.set_snr(ebn0_to_snr(EBN0, S, S, M))
+    link.update_distortion(ibo_val_db=w["ibo"])
+    link.set_snr(ebn0_to_snr(w["ebn0"], S, S, M))
     return link.engine()
 
 
-def cpu_baseline(seconds=15.0):
+def cpu_baseline(seconds=15.0, workload="2"):
     """The float64 oracle (oracle/sim.py, NumPy, one process / one core) on a bounded sample
     of the same workload: reported beside the GPU number, never the measured product."""
     from oracle import refmath as rm
     from oracle.sim import SimConfig, run_trials
-    cfg = SimConfig(A, S, F, M, pa="softlim", ibo_db=IBO, snr_db=float(rm.ebn0_to_snr(EBN0, S, S, M)))
+    w = WORKLOADS[workload]
+    cfg = SimConfig(w["A"], w["S"], w["F"], w["M"], pa=w["pa"], p_hardness=w["p"], ibo_db=w["ibo"],
+                    snr_db=float(rm.ebn0_to_snr(w["ebn0"], w["S"], w["S"], w["M"])))
     run_trials(cfg, 7, [0], iters=[0])  # warm caches / imports
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        run_trials(cfg, 7, np.arange(n, n + 16), iters=[0])
-        n += 16
+        step = 16 if w["F"] <= 2048 else 2
+        run_trials(cfg, 7, np.arange(n, n + step), iters=[0])
+        n += step
     dt = time.perf_counter() - t0
     return dict(value=round(n / dt, 3), unit="OFDM symbols/s", cores=1, kind="port",
-                sample=f"{n} trials of the config-2 chain (standard RX) through oracle/sim.py "
+                sample=f"{n} trials of the workload-{workload} chain (standard RX) through oracle/sim.py "
                        f"(NumPy float64, 1 process, {dt:.1f} s)")
 
 
@@ -108,6 +130,8 @@ def main():
     ap.add_argument("--iters", type=str, default="0", help="receiver iterations, e.g. 0 or 0,1,2,3,4")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--workload", default="2", choices=sorted(WORKLOADS),
+                    help="2 = BASELINE config 2 (headline); paper; 5su (config-5 array, one user)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -119,7 +143,8 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
-    eng = make_engine(local)
+    wl = WORKLOADS[args.workload]
+    eng = make_engine(local, args.workload)
     iters = [int(x) for x in args.iters.split(",")]
     B = args.batch
     seed = 2137
@@ -155,9 +180,9 @@ def main():
     total_trials = B * args.steps * world
     value = total_trials / dt
     avg_kernel_s = kern_ms / 1e3 / args.steps
-    b_alg = bytes_alg_per_trial() * B
-    f_alg = flops_alg_per_trial() * B
-    traffic, traffic_src = load_pmc_traffic(B)
+    b_alg = bytes_alg_per_trial(wl["A"], wl["S"], wl["F"]) * B
+    f_alg = flops_alg_per_trial(wl["A"], wl["S"], wl["F"]) * B
+    traffic, traffic_src = load_pmc_traffic(B) if args.workload == "2" else (None, None)
     out = {
         "metric": "OFDM symbols/s/GPU (64-ant,1024-sc) + achieved HBM %peak; BER match vs ref",
         "value": round(value, 1),
@@ -171,25 +196,24 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (on-device Philox bits / Rayleigh channel / AWGN)",
-        "config": {"workload": "BASELINE config 2: 64-ant MRT, 1024-sc (FFT 2048) 64-QAM, soft limiter IBO 3 dB, "
-                               "Rayleigh, Eb/N0 15 dB, standard RX",
+        "config": {"workload": wl["desc"] + (", standard RX" if iters == [0] else f", CNC iterations {iters}"),
                    "trials_per_gpu_per_step": B, "iters": iters, "parallelism": f"trial-sharded x{world}"},
         "roofline": {
             "bound": "mfma", "regime": "fp32 VALU (gfx950 f32 MFMA peak == f32 VALU peak)",
             "achieved": round(f_alg / avg_kernel_s / 1e12, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(f_alg / avg_kernel_s / 1e12 / FP32_PEAK_TFLOPS, 4),
             "traffic": traffic, "traffic_source": traffic_src,
-            "kernel": "mimo::trial_kernel<2048,128,8,aligned,rayleigh,no-csi,3 waves/SIMD,1 buffer,symbols in LDS>", "kernel_ms": round(avg_kernel_s * 1e3, 3),
-            "flops_alg_per_trial": flops_alg_per_trial(),
+            "kernel": "mimo::trial_kernel " + eng.describe(), "kernel_ms": round(avg_kernel_s * 1e3, 3),
+            "flops_alg_per_trial": flops_alg_per_trial(wl["A"], wl["S"], wl["F"]),
         },
         "hbm_alg": {"achieved": round(b_alg / avg_kernel_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(b_alg / avg_kernel_s / 1e9 / HBM_PEAK_GBS, 4),
-                    "bytes_alg_per_trial": bytes_alg_per_trial(),
+                    "bytes_alg_per_trial": bytes_alg_per_trial(wl["A"], wl["S"], wl["F"]),
                     "note": "SURVEY §8(d) staged-pipeline bytes; the fused kernel keeps them on chip"},
-        "ber": [round(float(x) / (total_trials * S * 6), 8) for x in err_tot],
+        "ber": [round(float(x) / (total_trials * wl["S"] * np.log2(wl["M"])), 8) for x in err_tot],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.workload)
     if dist:
         dist.destroy_process_group()
     if rank == 0:

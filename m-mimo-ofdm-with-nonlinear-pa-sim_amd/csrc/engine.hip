@@ -100,8 +100,10 @@ mimo::InstanceKey select_instance(const mimo_engine* e, bool csi) {
 }
 
 hipError_t launch(const mimo::InstanceKey& k, dim3 grid, hipStream_t st, const mimo::TrialParams& p, bool* found) {
-#ifdef MIMO_ONLY_F2048
-  if (k.F == 2048) return mimo::launch_trial_F2048(k, grid, st, p, found);
+#ifdef MIMO_ONLY_F  // single-size diagnostic / A-B builds (Makefile targets ablation, variant)
+#define MIMO_ONLY_CAT2(a, b) a##b
+#define MIMO_ONLY_CAT(a, b) MIMO_ONLY_CAT2(a, b)
+  if (k.F == MIMO_ONLY_F) return mimo::MIMO_ONLY_CAT(launch_trial_F, MIMO_ONLY_F)(k, grid, st, p, found);
   *found = false;
   return hipSuccess;
 #endif

@@ -188,7 +188,8 @@ struct TeamFft {
       const int jm = j & (NS - 1);
       if constexpr (NS > 1) {
         // [R][NS] block: uniform base per r (SGPRs) + the lane's jm as the VGPR offset
-        const float2* tws = tw + fft_tw_off(F, P, S);
+        constexpr int TW_OFF = fft_tw_off(F, P, S);  // forced compile-time (a runtime call otherwise)
+        const float2* tws = tw + TW_OFF;
 #pragma unroll
         for (int r = 1; r < R; ++r) {
           const float2 w = gload(tws + r * NS, jm);  // exp(-j 2 pi jm r / (NS R))

@@ -32,6 +32,9 @@ enum ChanKind : int { CH_RAYLEIGH = 1, CH_LOS = 2, CH_TWOPATH = 3 };
 enum RxKind : int { RX_CNC = 1, RX_MCNC = 2 };
 
 constexpr int kMaxWaves = 16;
+#ifndef MIMO_RAPP_INT
+#define MIMO_RAPP_INT 1
+#endif
 
 struct TrialParams {
   uint64_t seed;
@@ -175,6 +178,21 @@ __device__ __forceinline__ float2 pa_apply(int kind, float2 x, float sat, float 
   return make_float2(x.x * sc, x.y * sc);
 }
 
+// Rapp with an integer hardness: (pw/sat)^p by multiplication (config 5 uses p = 3),
+// one v_log + one v_exp per sample instead of two of each.
+template <int IP, int P>
+__device__ __forceinline__ void rapp_int(float2 (&d)[P], float inv_sat) {
+#pragma unroll
+  for (int m = 0; m < P; ++m) {
+    const float u = fmaf(d[m].x, d[m].x, d[m].y * d[m].y) * inv_sat;
+    float up = u;
+#pragma unroll
+    for (int i = 1; i < IP; ++i) up *= u;
+    const float sc = __builtin_amdgcn_exp2f((-0.5f / IP) * __builtin_amdgcn_logf(1.0f + up));
+    d[m] = make_float2(d[m].x * sc, d[m].y * sc);
+  }
+}
+
 // PA on all P samples of a thread: one uniform branch on the kind, then a straight loop.
 template <int P>
 __device__ __forceinline__ void pa_block(int kind, float2 (&d)[P], float sat, float sqrt_sat, float inv_sat,
@@ -182,6 +200,12 @@ __device__ __forceinline__ void pa_block(int kind, float2 (&d)[P], float sat, fl
   if (kind == PA_SOFTLIM) {
 #pragma unroll
     for (int m = 0; m < P; ++m) d[m] = pa_apply(PA_SOFTLIM, d[m], sat, sqrt_sat, inv_sat, rapp_p, toi);
+#if MIMO_RAPP_INT
+  } else if (kind == PA_RAPP && rapp_p == 3.0f) {
+    rapp_int<3>(d, inv_sat);
+  } else if (kind == PA_RAPP && rapp_p == 2.0f) {
+    rapp_int<2>(d, inv_sat);
+#endif
   } else if (kind == PA_RAPP) {
 #pragma unroll
     for (int m = 0; m < P; ++m) d[m] = pa_apply(PA_RAPP, d[m], sat, sqrt_sat, inv_sat, rapp_p, toi);
