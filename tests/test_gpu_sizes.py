@@ -1,0 +1,48 @@
+"""GPU parity across FFT sizes, team sizes, PA models and the generic (unaligned) slot path.
+
+Same tolerance as tests/test_gpu_engine.py (fp32 device vs float64 oracle on identical
+Philox inputs): >= 97 % of per-trial, per-iteration counts exact, totals within 2 % + 8.
+``MIMO_TEAM`` selects the alternative team size (engine.hip select_instance).
+"""
+import numpy as np
+import pytest
+
+from gpu_util import count_agreement, engine_for
+from oracle import sim
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # F,    S,    A, M,  pa,        p,   ibo, team
+    (2048, 1024, 8, 64, "softlim", 0.0, 3.0, 256),   # alternative 4-wave team (P = 8)
+    (4096, 2048, 8, 64, "softlim", 0.0, 3.0, None),  # paper-config FFT, 3 waves/SIMD profile
+    (4096, 2048, 8, 64, "softlim", 0.0, 3.0, 512),
+    (8192, 4096, 4, 64, "rapp", 3.0, 3.0, None),     # config-5 FFT / PA, integer-p Rapp path
+    (8192, 4096, 4, 16, "rapp", 2.5, 2.0, None),     # general Rapp path
+    (8192, 4096, 4, 64, "rapp", 3.0, 3.0, 1024),     # 16-wave team
+    (1024, 1000, 8, 16, "softlim", 0.0, 1.0, None),  # generic slots (S % 4T != 0)
+    (512, 256, 16, 4, "toi", 0.0, 5.0, None),        # QPSK, cubic PA
+    (2048, 1024, 8, 256, "softlim", 0.0, 0.0, None),  # 256-QAM at IBO 0 (strong clipping)
+]
+
+
+@pytest.mark.parametrize("F,S,A,M,pa,p,ibo,team", CASES)
+def test_sizes_vs_oracle(monkeypatch, F, S, A, M, pa, p, ibo, team):
+    if team is not None:
+        monkeypatch.setenv("MIMO_TEAM", str(team))
+    snr = float(sim.rm.ebn0_to_snr(14.0, S, S, M))
+    cfg = sim.SimConfig(A, S, F, M, pa=pa, p_hardness=p, ibo_db=ibo, snr_db=snr)
+    trials = np.arange(24)
+    iters = [0, 1, 2]
+    ref = sim.run_trials(cfg, 31, trials, iters=iters, incl_clean=True)
+    eng = engine_for(cfg)
+    err, bits, per = eng.run(31, 0, len(trials), iters, True, per_trial=True)
+    desc = eng.describe()
+    if team is not None:
+        assert f"T={team} " in desc, desc
+    agree = count_agreement(per, ref)
+    print(F, S, A, M, pa, p, ibo, desc, "agreement", agree, per.sum(0), ref.sum(0))
+    assert agree >= 0.97
+    np.testing.assert_allclose(per.sum(0), ref.sum(0), rtol=0.02, atol=8)
+    np.testing.assert_array_equal(err, per.sum(0))
+    assert all(int(b) == len(trials) * S * int(np.log2(M)) for b in bits)
