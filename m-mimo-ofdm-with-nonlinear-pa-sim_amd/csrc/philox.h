@@ -72,6 +72,15 @@ __device__ __forceinline__ void cn_pair(Key key, uint32_t q, uint32_t trial, uin
   z2 = box_muller(w.z, w.w, c);
 }
 
+// |z1|^2, |z2|^2 of cn_pair's draws without forming them: rho^2 = c log2(u1) (one v_log
+// per draw; no sqrt / sin / cos).  MRT norms only need the channel power.
+__device__ __forceinline__ void cn_pair_pow(Key key, uint32_t q, uint32_t trial, uint32_t stream, uint32_t aux,
+                                            float& p1, float& p2, float c = kNegLn2) {
+  const uint4 w = philox4x32_10(make_uint4(q, trial, stream, aux), key);
+  p1 = c * __builtin_amdgcn_logf(fmaf((float)w.x, 2.3283064365386963e-10f, 1.1641532182693481e-10f));
+  p2 = c * __builtin_amdgcn_logf(fmaf((float)w.z, 2.3283064365386963e-10f, 1.1641532182693481e-10f));
+}
+
 // Quarter pairing: sub-carrier k -> pair index q and slot (0: k1, 1: k2 = k1 + S/4).
 __device__ __forceinline__ void pair_of(int k, int n_sc, uint32_t& q, int& slot) {
   const int half = n_sc >> 1, quarter = n_sc >> 2;

@@ -33,7 +33,13 @@ enum RxKind : int { RX_CNC = 1, RX_MCNC = 2 };
 
 constexpr int kMaxWaves = 16;
 #ifndef MIMO_RAPP_INT
-#define MIMO_RAPP_INT 1
+#define MIMO_RAPP_INT 1   // A/B knobs (Makefile target variant); production defaults
+#endif
+#ifndef MIMO_PASS1_POW
+#define MIMO_PASS1_POW 1
+#endif
+#ifndef MIMO_ALPHA_POLY
+#define MIMO_ALPHA_POLY 1
 #endif
 
 struct TrialParams {
@@ -51,6 +57,10 @@ struct TrialParams {
   float sat_tx, sqrt_sat_tx, inv_sat_tx, rapp_p, toi_tx;
   float sat_cnc, sqrt_sat_cnc, inv_sat_cnc, toi_cnc, inv_alpha_cnc;
   float alpha_c;                 // 10^(IBO/10) S / A : gamma_a^2 = alpha_c / vk_pow[a]
+  // alpha(gamma_a^2) as a degree-8 polynomial in x = vk_pow[a] A / S - 1 on |x| <= alpha_xlim
+  // (host Chebyshev fit, ~1e-7 relative); the exact formula outside (engine.hip fit_alpha)
+  float apoly[9];
+  float inv_vk0, alpha_xlim;
   float es_over_snr;             // Es / 10^(SNR/10)
   float csi_a, csi_b;            // sqrt(1 - eps^2), eps
   float inv_sqrt_f;
@@ -289,6 +299,47 @@ struct Channel {
     }
   }
 
+  // |H|^2 of antenna a at the thread's slots (Rayleigh, FSPL factor f_rel left out as in
+  // gen<false>): the same draws as gen(), magnitudes only.
+  static __device__ __forceinline__ void power(const TrialParams& p, Key key, uint32_t trial, int a, int t,
+                                               float (&e2)[NSLOT]) {
+    const int S = p.n_sc;
+    const float sa = p.ant_rel[a];
+    const float c = kNegLn2 * (sa * sa);
+    if constexpr (ALIGNED) {
+      constexpr int Q = SL::HALF / 2;
+      const bool t0 = (t == 0);
+      const int qp = (S >> 2) - 1 + t;
+#pragma unroll
+      for (int j = 0; j < Q; ++j) {
+        float p1, p2;
+        const bool sw = (j == 0) && t0;
+        cn_pair_pow(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, ST_CHAN, (uint32_t)a, p1, p2,
+                    c);
+        e2[j] = sw ? p2 : p1;
+        e2[j + Q] = sw ? p1 : p2;
+        cn_pair_pow(key, (uint32_t)(t + T * j), trial, ST_CHAN, (uint32_t)a, p1, p2, c);
+        e2[SL::HALF + j] = p1;
+        e2[SL::HALF + j + Q] = p2;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) {
+        bool v;
+        const int k = SL::k_of(s, t, S, v);
+        e2[s] = 0.f;
+        if (v) {
+          uint32_t q;
+          int slot;
+          pair_of(k, S, q, slot);
+          float p1, p2;
+          cn_pair_pow(key, q, trial, ST_CHAN, (uint32_t)a, p1, p2, c);
+          e2[s] = slot == 0 ? p1 : p2;
+        }
+      }
+    }
+  }
+
   // True channel of antenna a at the thread's slots (relative scale: common factors
   // cancel in MRT, AGC and the SNR normalisation).  FREL = false leaves out the
   // per-sub-carrier FSPL factor fc/f_k, which the kernel then applies once per trial
@@ -432,6 +483,15 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   for (int s = 0; s < NSLOT; ++s) nrm2[s] = 0.f;
   for (int a = 0; a < (MIMO_ABL(p, ABL_PASS1) ? 1 : A); ++a) {
     const int tl = opaque(t);
+    if constexpr (CH == CH_RAYLEIGH && !CSI && MIMO_PASS1_POW) {
+      if (!MIMO_ABL(p, ABL_RNG)) {
+        float e2[NSLOT];
+        CHN::power(p, key, trial, a, tl, e2);
+#pragma unroll
+        for (int s = 0; s < NSLOT; ++s) nrm2[s] += e2[s];
+        continue;
+      }
+    }
     float2 h[NSLOT];
     CHN::template gen<FREL>(p, key, trial, a, tl, rx, h);
     if constexpr (CSI) {
@@ -531,7 +591,17 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         float vks = 0.f;
 #pragma unroll
         for (int i = 0; i < W; ++i) vks += vk_part[a & 1][i];
-        alpha_a = alpha_of_gamma2(p.alpha_c / vks);
+        const float x = fmaf(vks, p.inv_vk0, -1.0f);
+        // Polynomial alpha: -7 % at F = 2048, but +3 % at F = 8192 (SGPR pressure of the
+        // 8 waves/team instance, tools/ab_libs.py), so only up to F = 4096.
+        if (MIMO_ALPHA_POLY && F <= 4096 && fabsf(x) <= p.alpha_xlim) {
+          float acc = p.apoly[8];
+#pragma unroll
+          for (int i = 7; i >= 0; --i) acc = fmaf(acc, x, p.apoly[i]);
+          alpha_a = acc;
+        } else {
+          alpha_a = alpha_of_gamma2(p.alpha_c / vks);
+        }
       }
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
