@@ -284,7 +284,7 @@ int32_t mimo_engine_set_point(mimo_engine* e, const mimo_point* pt) {
   if (pt->pa_kind == MIMO_PA_RAPP && !(pt->p_hardness > 0)) return fail(MIMO_EINVAL, "p_hardness must be > 0");
   if (!(pt->cnc_alpha != 0)) return fail(MIMO_EINVAL, "cnc_alpha must be non-zero");
   if (pt->csi_eps >= 1.0) return fail(MIMO_EINVAL, "csi_eps must be < 1");
-  if (pt->csi_eps >= 0 && e->cfg.n_ant > 1024) return fail(MIMO_EINVAL, "CSI error supports n_ant <= 1024");
+  if (pt->csi_eps >= 0 && e->cfg.n_ant > mimo::kMaxCsiAnt) return fail(MIMO_EINVAL, "CSI error supports n_ant <= 512");
   e->pt = *pt;
   e->have_point = true;
   return MIMO_OK;

@@ -20,6 +20,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#ifndef MIMO_PAD0_SHIFT
+#define MIMO_PAD0_SHIFT 4
+#endif
+
 namespace mimo {
 
 // ---------------------------------------------------------------- compile-time trig
@@ -150,12 +154,17 @@ struct TeamFft {
   static constexpr int LOG_F = ilog2(F);
   static constexpr int LOG_P = ilog2(P);
   static constexpr int NST = fft_nst(F, P);
-  static constexpr int LDS_ELEMS = F + F / 32;
+  // Padding of exchange S: one slot per 2^PSH elements.  Exchange 0 (stage 0 writes
+  // 16t + r) uses 1/16 (MIMO_PAD0_SHIFT): it halves that exchange's modelled bank
+  // conflicts (tools/lds_conflicts.py); later exchanges use 1/32.
+  static constexpr int psh(int S) { return S == 0 ? MIMO_PAD0_SHIFT : 5; }
+  static constexpr int LDS_ELEMS = F + F / (1 << (MIMO_PAD0_SHIFT < 5 ? MIMO_PAD0_SHIFT : 5));
   static_assert((1 << LOG_F) == F && (1 << LOG_P) == P && P >= 2, "power-of-two sizes");
 
   static constexpr int bits(int s) { return fft_bits(F, P, s); }
   static constexpr int bits_before(int s) { return fft_bits_before(F, P, s); }
-  static __host__ __device__ constexpr int pad(int e) { return e + (e >> 5); }
+  template <int S>
+  static __host__ __device__ constexpr int pad(int e) { return e + (e >> psh(S)); }
   // Global-address-space load (the laundered table pointer would otherwise be generic
   // and compile to flat loads, which also count against lgkmcnt with the LDS traffic).
   static __device__ __forceinline__ float2 gload(const float2* p, int i) {
@@ -212,17 +221,17 @@ struct TeamFft {
         }
         // pad(base + r NS) == pad(base) + pad(r NS) for power-of-two NS, R, T (the
         // padding never splits a write group): one address per i, immediate offsets.
-        float2* wb = buf + pad((j / NS) * NS * R + jm);
+        float2* wb = buf + pad<S>((j / NS) * NS * R + jm);
 #pragma unroll
-        for (int r = 0; r < R; ++r) wb[pad(r * NS)] = v[r];
+        for (int r = 0; r < R; ++r) wb[pad<S>(r * NS)] = v[r];
       }
     }
     if constexpr (!LAST) {
       if (!no_xchg) {
         __syncthreads();
-        const float2* rb = buf + pad(t);
+        const float2* rb = buf + pad<S>(t);
 #pragma unroll
-        for (int m = 0; m < P; ++m) d[m] = rb[pad(T * m)];
+        for (int m = 0; m < P; ++m) d[m] = rb[pad<S>(T * m)];
       }
     }
   }

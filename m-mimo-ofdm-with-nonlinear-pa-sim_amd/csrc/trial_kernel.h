@@ -32,6 +32,7 @@ enum ChanKind : int { CH_RAYLEIGH = 1, CH_LOS = 2, CH_TWOPATH = 3 };
 enum RxKind : int { RX_CNC = 1, RX_MCNC = 2 };
 
 constexpr int kMaxWaves = 16;
+constexpr int kMaxCsiAnt = 512;  // CSI-error runs: antennas (LDS per team; engine.hip checks)
 #ifndef MIMO_RAPP_INT
 #define MIMO_RAPP_INT 1   // A/B knobs (Makefile target variant); production defaults
 #endif
@@ -428,7 +429,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   __shared__ float2 lds[FFT::LDS_TOTAL];
   __shared__ float red[kMaxWaves];
   __shared__ float vk_part[2][kMaxWaves];
-  __shared__ float pw_csi[CSI ? 1024 : 1];
+  __shared__ float pw_csi[CSI ? kMaxCsiAnt : 1];  // per-antenna mean |H|^2 (CSI model)
   __shared__ float2 symw_s[SYMW_LDS ? NSLOT * T : 1];  // [slot][thread]
 
   const int t = threadIdx.x;

@@ -10,7 +10,8 @@ REPO = __import__("os").path.dirname(__import__("os").path.dirname(__import__("o
 F = sys.argv[1]
 cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-fno-slp-vectorize",
        f"-DINST_F={F}", "-c", f"{REPO}/m-mimo-ofdm-with-nonlinear-pa-sim_amd/csrc/trial_inst.hip", "-o", "/tmp/rr.o",
-       "-Rpass-analysis=kernel-resource-usage"] + sys.argv[2:]
+       "-Rpass-analysis=kernel-resource-usage"] + (["-mllvm", "-amdgpu-sched-strategy=max-ilp"] if F == "2048" else []) \
+    + sys.argv[2:]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 rows, cur = [], None
 for line in out.splitlines():
