@@ -38,6 +38,8 @@ WORKLOADS = {
     "paper": dict(A=64, S=2048, F=4096, M=64, CP=128, pa="softlim", p=0.0, ibo=3.0, ebn0=15.0,
                   desc="paper config: 64-ant MRT, 2048-sc (FFT 4096) 64-QAM, soft limiter IBO 3 dB, Rayleigh, "
                        "Eb/N0 15 dB"),
+    "2gen": dict(A=64, S=1000, F=2048, M=64, CP=128, pa="softlim", p=0.0, ibo=3.0, ebn0=15.0,
+                 desc="config 2 with 1000 sub-carriers (generic, unaligned slot path)"),
     "5su": dict(A=256, S=4096, F=8192, M=64, CP=128, pa="rapp", p=3.0, ibo=3.0, ebn0=15.0,
                 desc="config-5 array at one user: 256-ant MRT, 4096-sc (FFT 8192) 64-QAM, Rapp p=3 IBO 3 dB, "
                      "Rayleigh, Eb/N0 15 dB"),

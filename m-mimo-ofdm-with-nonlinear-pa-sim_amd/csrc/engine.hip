@@ -125,14 +125,22 @@ int team_for(int F) { return mimo::team_size(F); }
 mimo::InstanceKey select_instance(const mimo_engine* e, bool csi) {
   mimo::InstanceKey k{};
   k.F = e->cfg.n_fft;
+  const int S = e->cfg.n_sub_carr;
+  auto aligned_at = [&](int T) {
+    const int P = k.F / T;
+    return (S % (4 * T) == 0) && S < k.F && (S / T == 8 || S / T == 4) && (S / T) < P;
+  };
   k.T = team_for(k.F);
+  // Unaligned bands (S % 4T != 0) run the generic predicated path with P slots per
+  // thread; the alternative team has half the points per thread, which measured 1.5x
+  // faster there (60.7 vs 40.7 ms at S = 1000, F = 2048; profiles/r01/ab_generic.json).
+  if (!aligned_at(k.T) && mimo::alt_team_size(k.F) != k.T) k.T = mimo::alt_team_size(k.F);
   if (const char* env = std::getenv("MIMO_TEAM")) {  // A/B override: MIMO_TEAM=<threads per trial>
     const int t = std::atoi(env);
     if (t == mimo::alt_team_size(k.F) || t == mimo::team_size(k.F)) k.T = t;
   }
-  const int S = e->cfg.n_sub_carr;
   const int P = k.F / k.T;
-  k.aligned = (S % (4 * k.T) == 0) && S < k.F && (S / k.T == 8 || S / k.T == 4) && (S / k.T) < P;
+  k.aligned = aligned_at(k.T);
   k.nslot = k.aligned ? S / k.T : P;
   k.ch = e->cfg.channel_kind;
   k.csi = csi;
