@@ -141,12 +141,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    # MIMO_BENCH_BACKEND=gloo rehearses the N > 1 path with ranks sharing the visible GPUs
+    # (device = LOCAL_RANK mod device count); the driver's runs use RCCL, one GPU per rank.
+    backend = os.environ.get("MIMO_BENCH_BACKEND", "nccl")
+    dev = local % max(1, torch.cuda.device_count())
+    tdev = f"cuda:{dev}" if backend == "nccl" else "cpu"
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(dev)
+        dist.init_process_group(backend)
     wl = WORKLOADS[args.workload]
-    eng = make_engine(local, args.workload)
+    eng = make_engine(dev, args.workload)
     iters = [int(x) for x in args.iters.split(",")]
     B = args.batch
     seed = 2137
@@ -173,10 +178,10 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
+        t = torch.tensor([dt], device=tdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        c = torch.tensor(err_tot.astype(np.int64), device=f"cuda:{local}")
+        c = torch.tensor(err_tot.astype(np.int64), device=tdev)
         dist.all_reduce(c)
         err_tot = c.cpu().numpy()
     total_trials = B * args.steps * world
