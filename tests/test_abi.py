@@ -1,0 +1,89 @@
+"""The C-ABI boundary on a machine without a GPU: the library loads, exports every entry
+point include/mimo_engine.h declares, and validates configurations host-side with the
+reference's error messages (no HIP call happens before the first compute call)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import _engine
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "mimo_engine.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mimo_\w+)\s*\(", text)))
+
+
+def test_header_and_binding_agree():
+    names = declared_functions()
+    assert len(names) >= 20
+    assert sorted(_engine.SYMBOLS) == names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _engine.lib()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    assert lib.mimo_abi_version() == 1
+
+
+def _cfg(**kw):
+    tx = np.zeros((kw.get("n_ant", 4), 3))
+    fr = np.full(kw.get("n_fft", 256), 3.5e9)
+    base = dict(n_ant=4, n_sub_carr=128, n_fft=256, constel_size=16, cp_len=16, channel_kind=1, receiver_kind=1,
+                device=-1, rx_loc_var=10.0, reroll_chan=1, reserved=0)
+    base.update(kw)
+    c = _engine.MimoConfig(**base, tx_pos=tx.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                           carrier_freqs=fr.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return c, (tx, fr)
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(n_fft=300), "n_fft must be a power of two"),
+    (dict(n_fft=16384), "n_fft must be a power of two"),
+    (dict(n_sub_carr=256), "n_sub_carr must be a multiple of 4"),
+    (dict(n_sub_carr=126), "n_sub_carr must be a multiple of 4"),
+    (dict(constel_size=8), "only square QAM supported"),      # modulation.py:236-237
+    (dict(constel_size=36), "only square QAM supported"),
+    (dict(n_ant=0), "n_ant must be in"),
+    (dict(channel_kind=7), "unknown channel_kind"),
+    (dict(receiver_kind=0), "unknown receiver_kind"),
+])
+def test_create_rejects_invalid_configs(kw, msg):
+    lib = _engine.lib()
+    c, keep = _cfg(**kw)
+    h = lib.mimo_engine_create(ctypes.byref(c))
+    assert not h
+    assert msg in lib.mimo_last_error().decode()
+
+
+def test_valid_engine_is_host_only_until_run():
+    """create / set_point / describe / destroy never touch HIP (fork safety)."""
+    lib = _engine.lib()
+    c, keep = _cfg(n_fft=512, n_sub_carr=256)
+    h = lib.mimo_engine_create(ctypes.byref(c))
+    assert h
+    pt = _engine.MimoPoint(ibo_db=3.0, snr_db=20.0, avg_symbol_power=10.0, pa_kind=1, cnc_pa_kind=1, sat_pow=1.0,
+                           p_hardness=0.0, toi_coeff=0.0, cnc_sat_pow=1.0, cnc_toi_coeff=0.0, cnc_alpha=0.9,
+                           csi_eps=-1.0)
+    assert lib.mimo_engine_set_point(h, ctypes.byref(pt)) == 0
+    desc = lib.mimo_engine_describe(h).decode()
+    assert "F=512" in desc and "aligned" in desc, desc
+    bad = _engine.MimoPoint(**{f: getattr(pt, f) for f, _ in _engine.MimoPoint._fields_})
+    bad.csi_eps = 1.5
+    assert lib.mimo_engine_set_point(h, ctypes.byref(bad)) == -1  # MIMO_EINVAL
+    assert "csi_eps" in lib.mimo_last_error().decode()
+    lib.mimo_engine_destroy(h)
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(_engine, "_lib", None)
+    monkeypatch.setattr(_engine, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(_engine.EngineError, match="not found"):
+        _engine.lib()
