@@ -20,6 +20,12 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#ifndef MIMO_DIAG_NOPREBAR
+#define MIMO_DIAG_NOPREBAR 0  // timing diagnostics only (wrong results); production = 0
+#endif
+#ifndef MIMO_DIAG_NOTW
+#define MIMO_DIAG_NOTW 0
+#endif
 #ifndef MIMO_PAD0_SHIFT
 #define MIMO_PAD0_SHIFT 4
 #endif
@@ -167,10 +173,80 @@ struct TeamFft {
   static __host__ __device__ constexpr int pad(int e) { return e + (e >> psh(S)); }
   // Global-address-space load (the laundered table pointer would otherwise be generic
   // and compile to flat loads, which also count against lgkmcnt with the LDS traffic).
+  static __device__ __forceinline__ float2 opaque_tw(int r) {
+    float2 w = make_float2(0.6f, 0.8f * (float)(r & 1));
+    asm volatile("" : "+v"(w.x), "+v"(w.y));
+    return w;
+  }
   static __device__ __forceinline__ float2 gload(const float2* p, int i) {
     typedef float v2f __attribute__((ext_vector_type(2)));
     const v2f v = ((const __attribute__((address_space(1))) v2f*)p)[i];
     return make_float2(v.x, v.y);
+  }
+
+  // Twiddles of stage S for butterflies i > 0: jm_i = jm_0 + OFF_i with OFF_i = (T i) mod NS
+  // (T and NS are powers of two, t < T), so w_i[r] = w_0[r] exp(-j 2 pi OFF_i r / (NS R)):
+  // a compile-time rotation instead of a load.
+  template <int N, int OFF, int R, int r = 1>
+  static __device__ __forceinline__ void tw_shift(float2 (&w)[R], const float2 (&w0)[R]) {
+    if constexpr (r < R) {
+      w[r] = ctw<OFF * r, N, -1>(w0[r]);
+      tw_shift<N, OFF, R, r + 1>(w, w0);
+    }
+  }
+
+  // One radix-R butterfly (index i of the thread's B) of stage S.
+  template <int S, int DIR, int I>
+  static __device__ __forceinline__ void butterfly(float2 (&d)[P], float2* buf, const float2 (&w0)[1 << bits(S)],
+                                                   int t, bool no_xchg) {
+    constexpr int R = 1 << bits(S);
+    constexpr int NS = 1 << bits_before(S);
+    constexpr int B = P / R;
+    constexpr bool LAST = (S == NST - 1);
+    float2 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = d[I + r * B];
+    const int j = t + T * I;
+    const int jm = j & (NS - 1);
+    if constexpr (NS > 1) {
+      constexpr int OFF = (T * I) & (NS - 1);
+      float2 w[R];
+      if constexpr (OFF == 0) {
+#pragma unroll
+        for (int r = 1; r < R; ++r) w[r] = w0[r];
+      } else {
+        tw_shift<NS * R, OFF, R>(w, w0);
+      }
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[r] = DIR < 0 ? cmul(v[r], w[r]) : cmulc(v[r], w[r]);
+    }
+    Dft<R, DIR>::run(v);
+    if constexpr (LAST) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) d[I + r * B] = v[r];
+    } else if (no_xchg) {  // ablation: data stay in registers (wrong result, no LDS / barriers)
+#pragma unroll
+      for (int r = 0; r < R; ++r) d[I + r * B] = v[r];
+    } else {
+      // One buffer: everyone must have read the previous exchange before it is
+      // overwritten.  The barrier sits after this stage's twiddle loads and DFT, so
+      // their latency overlaps the previous exchange's reads.
+      if constexpr (NBUF == 1 && I == 0 && !MIMO_DIAG_NOPREBAR) __syncthreads();
+      // pad(base + r NS) == pad(base) + pad(r NS) for power-of-two NS, R, T (the
+      // padding never splits a write group): one address per i, immediate offsets.
+      float2* wb = buf + pad<S>((j / NS) * NS * R + jm);
+#pragma unroll
+      for (int r = 0; r < R; ++r) wb[pad<S>(r * NS)] = v[r];
+    }
+  }
+
+  template <int S, int DIR, int I = 0>
+  static __device__ __forceinline__ void butterflies(float2 (&d)[P], float2* buf, const float2 (&w0)[1 << bits(S)],
+                                                     int t, bool no_xchg) {
+    if constexpr (I < P / (1 << bits(S))) {
+      butterfly<S, DIR, I>(d, buf, w0, t, no_xchg);
+      butterflies<S, DIR, I + 1>(d, buf, w0, t, no_xchg);
+    }
   }
 
   // Exchange buffers alternate (stage S of a transform started at parity PAR uses buffer
@@ -179,6 +255,12 @@ struct TeamFft {
   // of exchange k+1, which every thread reaches only after reading X for exchange k.
   // One barrier per exchange.  Callers keep the number of exchanges between two
   // transforms' parities consistent (an antenna = IFFT + FFT = an even count).
+  //
+  // Twiddles: the [R][NS] block of stage S gives w(jm, r) = exp(-j 2 pi jm r / (NS R)).
+  // Only r = 1, 2, 4, ... are loaded (uniform base per r in SGPRs + the lane's jm as the
+  // VGPR offset); the other r are products w(jm, a) w(jm, b), a + b = r (at most
+  // log2 R - 1 roundings).  Loads, not multiplies, were the twiddles' cost: dropping the
+  // loads saved 17 % of the kernel, dropping the multiplies 8 % (profiles/r01).
   template <int S, int DIR, int PAR>
   static __device__ __forceinline__ void stage(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
                                                bool no_xchg) {
@@ -188,44 +270,25 @@ struct TeamFft {
     constexpr bool LAST = (S == NST - 1);
     static_assert(B >= 1 && B * R == P, "radix must divide points per thread");
     float2* buf = lds + (NBUF == 2 ? ((S + PAR) & 1) * LDS_ELEMS : 0);
+    float2 w0[R];
+    if constexpr (NS > 1) {
+      constexpr int TW_OFF = fft_tw_off(F, P, S);  // forced compile-time (a runtime call otherwise)
+      const float2* tws = tw + TW_OFF;
+      const int jm0 = t & (NS - 1);
 #pragma unroll
-    for (int i = 0; i < B; ++i) {
-      float2 v[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) v[r] = d[i + r * B];
-      const int j = t + T * i;
-      const int jm = j & (NS - 1);
-      if constexpr (NS > 1) {
-        // [R][NS] block: uniform base per r (SGPRs) + the lane's jm as the VGPR offset
-        constexpr int TW_OFF = fft_tw_off(F, P, S);  // forced compile-time (a runtime call otherwise)
-        const float2* tws = tw + TW_OFF;
-#pragma unroll
-        for (int r = 1; r < R; ++r) {
-          const float2 w = gload(tws + r * NS, jm);  // exp(-j 2 pi jm r / (NS R))
-          v[r] = DIR < 0 ? cmul(v[r], w) : cmulc(v[r], w);
+      for (int r = 1; r < R; ++r) {
+        if ((r & (r - 1)) == 0) {
+          w0[r] = MIMO_DIAG_NOTW == 1 ? make_float2(1.f, 0.f)  // diagnostic: no twiddle traffic
+                  : MIMO_DIAG_NOTW == 2 ? opaque_tw(r)            // diagnostic: multiplies, no loads
+                                        : gload(tws + r * NS, jm0);
+        } else {
+          int hb = r;
+          while (hb & (hb - 1)) hb &= hb - 1;  // highest power of two below r (unrolled: constant)
+          w0[r] = cmul(w0[hb], w0[r - hb]);
         }
-      }
-      Dft<R, DIR>::run(v);
-      if constexpr (LAST) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) d[i + r * B] = v[r];
-      } else if (no_xchg) {  // ablation: data stay in registers (wrong result, no LDS / barriers)
-#pragma unroll
-        for (int r = 0; r < R; ++r) d[i + r * B] = v[r];
-      } else {
-        // One buffer: everyone must have read the previous exchange before it is
-        // overwritten.  The barrier sits after this stage's twiddle loads and DFT, so
-        // their latency overlaps the previous exchange's reads.
-        if constexpr (NBUF == 1) {
-          if (i == 0) __syncthreads();
-        }
-        // pad(base + r NS) == pad(base) + pad(r NS) for power-of-two NS, R, T (the
-        // padding never splits a write group): one address per i, immediate offsets.
-        float2* wb = buf + pad<S>((j / NS) * NS * R + jm);
-#pragma unroll
-        for (int r = 0; r < R; ++r) wb[pad<S>(r * NS)] = v[r];
       }
     }
+    butterflies<S, DIR>(d, buf, w0, t, no_xchg);
     if constexpr (!LAST) {
       if (!no_xchg) {
         __syncthreads();
