@@ -26,6 +26,9 @@
 #ifndef MIMO_DIAG_NOTW
 #define MIMO_DIAG_NOTW 0
 #endif
+#ifndef MIMO_TW_LOAD_MAX
+#define MIMO_TW_LOAD_MAX 64  // twiddle powers r <= this are loaded (1: square the rest; measured neutral)
+#endif
 #ifndef MIMO_PAD0_SHIFT
 #define MIMO_PAD0_SHIFT 4
 #endif
@@ -277,10 +280,13 @@ struct TeamFft {
       const int jm0 = t & (NS - 1);
 #pragma unroll
       for (int r = 1; r < R; ++r) {
-        if ((r & (r - 1)) == 0) {
-          w0[r] = MIMO_DIAG_NOTW == 1 ? make_float2(1.f, 0.f)  // diagnostic: no twiddle traffic
+        if (r == 1 || ((r & (r - 1)) == 0 && r > MIMO_TW_LOAD_MAX)) {
+          w0[r] = r > 1 ? cmul(w0[r / 2], w0[r / 2])  // w(2r) = w(r)^2
+                  : MIMO_DIAG_NOTW == 1 ? make_float2(1.f, 0.f)  // diagnostic: no twiddle traffic
                   : MIMO_DIAG_NOTW == 2 ? opaque_tw(r)            // diagnostic: multiplies, no loads
                                         : gload(tws + r * NS, jm0);
+        } else if ((r & (r - 1)) == 0) {
+          w0[r] = gload(tws + r * NS, jm0);
         } else {
           int hb = r;
           while (hb & (hb - 1)) hb &= hb - 1;  // highest power of two below r (unrolled: constant)
