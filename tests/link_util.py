@@ -38,3 +38,10 @@ def build_link(n_ant=8, n_sc=64, n_fft=128, M=16, cp=4, pa="softlim", ibo=1.0, p
                          csi_epsylon=csi, **kw)
     link.update_distortion(ibo_val_db=ibo)
     return link, mod
+
+
+def simulate_child(link, seed_arr, err, bits, iters=(0, 1)):
+    """Target of a spawned worker: what a reference driver's mp.Process runs
+    (main_mp_miso_cnc_ber_vs_ebn0.py:122-132)."""
+    import numpy as np
+    link.simulate(True, True, np.asarray(iters), seed_arr, err, bits)

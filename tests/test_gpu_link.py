@@ -82,3 +82,32 @@ def test_sweep_grid_on_gpu_equals_per_point_runs():
     ber = sweep.ber_from_counts(err, bits)
     assert np.all(np.diff(ber[:, :, 1], axis=1) <= 0)  # BER falls with Eb/N0
     assert np.all(bits[..., 0] >= 1024 * 64) or np.all(err[..., 0] >= 500)
+
+
+def test_workers_share_counters_like_the_reference_drivers():
+    """Two worker processes run Link.simulate into shared mp.Array counters, as the
+    reference's drivers do (mp.Process per core, mp_model.py:181-187).  'spawn' because
+    this pytest process already holds a HIP context; the drivers fork before any HIP use
+    (Link construction is HIP-free, tests/test_link_host.py)."""
+    import link_util
+    ctx = mp.get_context("spawn")
+    per_sym = 256 * 4
+    bmax = per_sym * 3000
+    link, _ = build_link(n_ant=8, n_sc=256, n_fft=512, M=16, ibo=1.0, bits_sent_max=bmax, n_err_min=10 ** 12)
+    link.set_snr(14.0)
+    link.max_batch = 512
+    err, bits = ctx.Array(ctypes.c_double, 3, lock=True), ctx.Array(ctypes.c_double, 3, lock=True)
+    procs = [ctx.Process(target=link_util.simulate_child, args=(link, [s, 5, 6], err, bits)) for s in (1, 2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert [p.exitcode for p in procs] == [0, 0]
+    e, b = np.asarray(err[:]), np.asarray(bits[:])
+    assert np.all(b >= bmax) and np.all(b <= bmax + 2 * 512 * per_sym), b
+    # one process, same point: the BERs agree within sampling error
+    err1, bits1 = shared(3)
+    link.simulate(True, True, np.array([0, 1]), [3, 5, 6], err1, bits1)
+    ber, ber1 = e / b, np.asarray(err1[:]) / np.asarray(bits1[:])
+    sig = np.sqrt(ber1 / b) * 4 + 1e-6
+    assert np.all(np.abs(ber - ber1) < 6 * sig), (ber, ber1)
