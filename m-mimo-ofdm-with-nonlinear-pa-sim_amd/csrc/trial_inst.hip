@@ -12,6 +12,9 @@ namespace mimo {
 namespace {
 
 constexpr int kF = INST_F;
+#ifndef MIMO_TWOPATH_W2
+#define MIMO_TWOPATH_W2 0  // 1: two-path at 2 waves/SIMD (measured 12 % slower than 3)
+#endif
 #ifndef MIMO_MINW16
 #define MIMO_MINW16 3  // waves/SIMD target of the 16-point aligned instances (A/B knob)
 #endif
@@ -31,7 +34,7 @@ struct Profile {
 constexpr Profile profile_for(int T, bool aligned, int ch) {
   const int P = kF / T;
   if (!aligned) return Profile{2, kF >= 8192 ? 1 : 2, true};
-  if (ch == CH_TWOPATH) return Profile{2, 2, false};  // fp64 geometry per antenna: register-heavy
+  if (ch == CH_TWOPATH && MIMO_TWOPATH_W2) return Profile{2, 2, false};  // fp64 geometry: register-heavy
   if (P < 16) return Profile{4, 2, false};
   if (kF <= 4096) return Profile{MIMO_MINW16, MIMO_MINW16 == 3 ? 1 : 2, MIMO_MINW16 == 3};
   return Profile{2, 2, false};

@@ -374,11 +374,11 @@ struct Channel {
       double d_sec = 0.0;
       float att_sec = 0.f;
       if constexpr (CH == CH_TWOPATH) {
-        // channel.py:138-147: elevation from the mirrored geometry
-        const double horiz = sqrt(dx * dx + dy * dy);
-        const double elev = atan((tz + rx[2]) / horiz);
-        const double se = sin(elev);
-        d_sec = tz / se + rx[2] / se;
+        // channel.py:138-147: elevation from the mirrored geometry, d_sec = tz/sin(el) +
+        // rz/sin(el) with el = atan((tz + rz) / horiz), i.e. the mirrored path length
+        // sqrt(horiz^2 + (tz + rz)^2) (no fp64 atan / sin; equal to ~1e-16 relative)
+        const double hz = tz + rx[2];
+        d_sec = sqrt(dx * dx + dy * dy + hz * hz);
         att_sec = (float)(p.d0 / d_sec);
       }
 #pragma unroll
