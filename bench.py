@@ -46,6 +46,8 @@ WORKLOADS = {
                      desc="config 2 geometry over the two-path channel"),
     "2mcnc": dict(A=64, S=1024, F=2048, M=64, CP=128, pa="softlim", p=0.0, ibo=3.0, ebn0=15.0, mcnc=True,
                   desc="config 2 with the MCNC receiver (one full array pass per iteration)"),
+    "2csi": dict(A=64, S=1024, F=2048, M=64, CP=128, pa="softlim", p=0.0, ibo=3.0, ebn0=15.0, csi=0.1,
+                 desc="config 2 with imperfect CSI (epsilon 0.1, mp_model.py:253-288)"),
     "5su": dict(A=256, S=4096, F=8192, M=64, CP=128, pa="rapp", p=3.0, ibo=3.0, ebn0=15.0,
                 desc="config-5 array at one user: 256-ant MRT, 4096-sc (FFT 8192) 64-QAM, Rapp p=3 IBO 3 dB, "
                      "Rayleigh, Eb/N0 15 dB"),
@@ -96,7 +98,7 @@ def make_engine(device, workload="2"):
         ch.calc_channel_mat(tx_transceivers=arr.array_elements, rx_transceiver=rx, skip_attenuation=False)
     link = mp_model.Link(mod_obj=mod, array_obj=arr, std_rx_obj=rx, chan_obj=ch, noise_obj=noise.Awgn(snr_db=10),
                          rx_loc_var=10.0, n_err_min=10 ** 12, bits_sent_max=10 ** 15, is_mcnc=w.get("mcnc", False),
-                         device=device)
+                         csi_epsylon=w.get("csi"), device=device)
     link.update_distortion(ibo_val_db=w["ibo"])
     link.set_snr(ebn0_to_snr(w["ebn0"], S, S, M))
     return link.engine()
@@ -110,7 +112,7 @@ def cpu_baseline(seconds=15.0, workload="2"):
     w = WORKLOADS[workload]
     cfg = SimConfig(w["A"], w["S"], w["F"], w["M"], pa=w["pa"], p_hardness=w["p"], ibo_db=w["ibo"],
                     snr_db=float(rm.ebn0_to_snr(w["ebn0"], w["S"], w["S"], w["M"])), channel=w.get("chan", "rayleigh"),
-                    receiver="mcnc" if w.get("mcnc") else "cnc")
+                    receiver="mcnc" if w.get("mcnc") else "cnc", csi_eps=w.get("csi"))
     run_trials(cfg, 7, [0], iters=[0])  # warm caches / imports
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
