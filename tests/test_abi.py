@@ -87,3 +87,42 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_engine, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_engine.EngineError, match="not found"):
         _engine.lib()
+
+
+def _engine_with_point():
+    lib = _engine.lib()
+    c, keep = _cfg(n_fft=512, n_sub_carr=256)
+    h = lib.mimo_engine_create(ctypes.byref(c))
+    pt = _engine.MimoPoint(ibo_db=3.0, snr_db=20.0, avg_symbol_power=10.0, pa_kind=1, cnc_pa_kind=1, sat_pow=1.0,
+                           p_hardness=0.0, toi_coeff=0.0, cnc_sat_pow=1.0, cnc_toi_coeff=0.0, cnc_alpha=0.9,
+                           csi_eps=-1.0)
+    assert lib.mimo_engine_set_point(h, ctypes.byref(pt)) == 0
+    return lib, h, pt, keep
+
+
+@pytest.mark.parametrize("iters,first,n,msg", [
+    ([2, 1], 0, 8, "sorted and unique"),
+    ([1, 1], 0, 8, "sorted and unique"),
+    ([32], 0, 8, "[0, 31]"),
+    ([-1], 0, 8, "[0, 31]"),
+    ([], 0, 8, "at least one iteration"),
+    ([0], (1 << 32) - 4, 8, "fit 32 bits"),
+])
+def test_run_validates_arguments_before_any_hip_call(iters, first, n, msg):
+    lib, h, pt, keep = _engine_with_point()
+    it = np.asarray(iters, np.int32)
+    err = np.zeros(4, np.uint64)
+    bits = np.zeros(4, np.uint64)
+    u64 = ctypes.POINTER(ctypes.c_uint64)
+    rc = lib.mimo_engine_run(h, 1, first, n, it.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(it), 0,
+                             err.ctypes.data_as(u64), bits.ctypes.data_as(u64), None)
+    assert rc == -1 and msg in lib.mimo_last_error().decode()
+    # before set_point
+    c, keep2 = _cfg(n_fft=512, n_sub_carr=256)
+    h2 = lib.mimo_engine_create(ctypes.byref(c))
+    it0 = np.zeros(1, np.int32)
+    rc = lib.mimo_engine_run(h2, 1, 0, 8, it0.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), 1, 0,
+                             err.ctypes.data_as(u64), bits.ctypes.data_as(u64), None)
+    assert rc == -1 and "set_point" in lib.mimo_last_error().decode()
+    lib.mimo_engine_destroy(h)
+    lib.mimo_engine_destroy(h2)

@@ -80,3 +80,19 @@ def test_trial_index_invariance():
     _, _, a = eng.run(5, 0, 300, [0, 2], True, per_trial=True)
     _, _, b = eng.run(5, 100, 100, [0, 2], True, per_trial=True)
     np.testing.assert_array_equal(a[100:200], b)
+
+
+def test_edge_cases_empty_subsets_and_index_limits():
+    """Empty batches add nothing; an iteration subset equals the same columns of a fuller
+    run; trial indices up to 2^32 - 1 are valid (the Philox counter word is 32 bits)."""
+    cfg = sim.SimConfig(8, 256, 512, 16, ibo_db=1.0, snr_db=12.0)
+    eng = engine_for(cfg)
+    e0, b0, p0 = eng.run(3, 0, 0, [0], True, per_trial=True)
+    assert e0.tolist() == [0, 0] and b0.tolist() == [0, 0] and p0.shape == (0, 2)
+    _, _, full = eng.run(3, 10, 64, [0, 2, 4], True, per_trial=True)
+    _, _, sub = eng.run(3, 10, 64, [2, 4], False, per_trial=True)
+    np.testing.assert_array_equal(sub, full[:, 2:])
+    top = (1 << 32) - 16
+    e, b, per = eng.run(3, top, 16, [0], False, per_trial=True)
+    ref = sim.run_trials(cfg, 3, np.arange(top, top + 16), iters=[0])
+    assert count_agreement(per, ref) >= 0.97
