@@ -99,33 +99,64 @@ __device__ __forceinline__ float2 ctw(float2 x) {
   }
 }
 
+// a + b / a - b where inputs known to be zero at compile time (ZA, ZB) are skipped:
+// pruning the IFFT's structurally-zero out-of-band inputs.
+template <bool ZA, bool ZB>
+__device__ __forceinline__ float2 zadd(float2 a, float2 b) {
+  if constexpr (ZA && ZB) return make_float2(0.f, 0.f);
+  else if constexpr (ZA) return b;
+  else if constexpr (ZB) return a;
+  else return cadd(a, b);
+}
+template <bool ZA, bool ZB>
+__device__ __forceinline__ float2 zsub(float2 a, float2 b) {
+  if constexpr (ZA && ZB) return make_float2(0.f, 0.f);
+  else if constexpr (ZA) return make_float2(-b.x, -b.y);
+  else if constexpr (ZB) return a;
+  else return csub(a, b);
+}
+
 // In-register DFT of size R (natural order in and out), four-step R = R1 x R2.
-template <int R, int DIR>
+// ZM: bit n set = input n is zero for every thread (compile-time pruning).
+template <int R, int DIR, uint32_t ZM = 0>
 struct Dft {
+  static constexpr bool z(int n) { return ((ZM >> n) & 1u) != 0; }
+  static constexpr uint32_t sub_mask(int n1, int r1, int r2) {
+    uint32_t m = 0;
+    for (int n2 = 0; n2 < r2; ++n2) m |= ((ZM >> (n1 + r1 * n2)) & 1u) << n2;
+    return m;
+  }
+  template <int N1, int R1, int R2>
+  static __device__ __forceinline__ void first_level(float2 (&sub)[R1][R2], const float2* v) {
+    if constexpr (N1 < R1) {
+#pragma unroll
+      for (int n2 = 0; n2 < R2; ++n2) sub[N1][n2] = v[N1 + R1 * n2];
+      Dft<R2, DIR, sub_mask(N1, R1, R2)>::run(sub[N1]);
+      first_level<N1 + 1, R1, R2>(sub, v);
+    }
+  }
+
   static __device__ __forceinline__ void run(float2* v) {
     if constexpr (R == 1) {
       return;
     } else if constexpr (R == 2) {
       const float2 a = v[0], b = v[1];
-      v[0] = cadd(a, b);
-      v[1] = csub(a, b);
+      v[0] = zadd<z(0), z(1)>(a, b);
+      v[1] = zsub<z(0), z(1)>(a, b);
     } else if constexpr (R == 4) {
-      const float2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
-      const float2 t2 = cadd(v[1], v[3]), t3 = ctw<1, 4, DIR>(csub(v[1], v[3]));
-      v[0] = cadd(t0, t2);
-      v[2] = csub(t0, t2);
-      v[1] = cadd(t1, t3);
-      v[3] = csub(t1, t3);
+      constexpr bool z02 = z(0) && z(2), z13 = z(1) && z(3);
+      const float2 t0 = zadd<z(0), z(2)>(v[0], v[2]), t1 = zsub<z(0), z(2)>(v[0], v[2]);
+      const float2 t2 = zadd<z(1), z(3)>(v[1], v[3]);
+      const float2 t3 = z13 ? make_float2(0.f, 0.f) : ctw<1, 4, DIR>(zsub<z(1), z(3)>(v[1], v[3]));
+      v[0] = zadd<z02, z13>(t0, t2);
+      v[2] = zsub<z02, z13>(t0, t2);
+      v[1] = zadd<z02, z13>(t1, t3);
+      v[3] = zsub<z02, z13>(t1, t3);
     } else {
       constexpr int R1 = (R >= 16) ? 4 : 2;
       constexpr int R2 = R / R1;
       float2 sub[R1][R2];
-#pragma unroll
-      for (int n1 = 0; n1 < R1; ++n1) {
-#pragma unroll
-        for (int n2 = 0; n2 < R2; ++n2) sub[n1][n2] = v[n1 + R1 * n2];
-        Dft<R2, DIR>::run(sub[n1]);
-      }
+      first_level<0, R1, R2>(sub, v);
       Twid<R1, R2, 1, 0>::apply(sub);
 #pragma unroll
       for (int k2 = 0; k2 < R2; ++k2) {
@@ -199,7 +230,14 @@ struct TeamFft {
   }
 
   // One radix-R butterfly (index i of the thread's B) of stage S.
-  template <int S, int DIR, int I>
+  // Zero mask of butterfly I's inputs v[r] = d[I + r B] from the register mask ZM.
+  static constexpr uint32_t bfly_mask(uint32_t zm, int i, int b, int r) {
+    uint32_t m = 0;
+    for (int k = 0; k < r; ++k) m |= ((zm >> (i + k * b)) & 1u) << k;
+    return m;
+  }
+
+  template <int S, int DIR, int I, uint32_t ZM>
   static __device__ __forceinline__ void butterfly(float2 (&d)[P], float2* buf, const float2 (&w0)[1 << bits(S)],
                                                    int t, bool no_xchg) {
     constexpr int R = 1 << bits(S);
@@ -223,7 +261,7 @@ struct TeamFft {
 #pragma unroll
       for (int r = 1; r < R; ++r) v[r] = DIR < 0 ? cmul(v[r], w[r]) : cmulc(v[r], w[r]);
     }
-    Dft<R, DIR>::run(v);
+    Dft<R, DIR, (S == 0 ? bfly_mask(ZM, I, B, R) : 0u)>::run(v);
     if constexpr (LAST) {
 #pragma unroll
       for (int r = 0; r < R; ++r) d[I + r * B] = v[r];
@@ -243,12 +281,12 @@ struct TeamFft {
     }
   }
 
-  template <int S, int DIR, int I = 0>
+  template <int S, int DIR, uint32_t ZM, int I = 0>
   static __device__ __forceinline__ void butterflies(float2 (&d)[P], float2* buf, const float2 (&w0)[1 << bits(S)],
                                                      int t, bool no_xchg) {
     if constexpr (I < P / (1 << bits(S))) {
-      butterfly<S, DIR, I>(d, buf, w0, t, no_xchg);
-      butterflies<S, DIR, I + 1>(d, buf, w0, t, no_xchg);
+      butterfly<S, DIR, I, ZM>(d, buf, w0, t, no_xchg);
+      butterflies<S, DIR, ZM, I + 1>(d, buf, w0, t, no_xchg);
     }
   }
 
@@ -264,7 +302,7 @@ struct TeamFft {
   // VGPR offset); the other r are products w(jm, a) w(jm, b), a + b = r (at most
   // log2 R - 1 roundings).  Loads, not multiplies, were the twiddles' cost: dropping the
   // loads saved 17 % of the kernel, dropping the multiplies 8 % (profiles/r01).
-  template <int S, int DIR, int PAR>
+  template <int S, int DIR, int PAR, uint32_t ZM>
   static __device__ __forceinline__ void stage(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
                                                bool no_xchg) {
     constexpr int R = 1 << bits(S);
@@ -294,7 +332,7 @@ struct TeamFft {
         }
       }
     }
-    butterflies<S, DIR>(d, buf, w0, t, no_xchg);
+    butterflies<S, DIR, ZM>(d, buf, w0, t, no_xchg);
     if constexpr (!LAST) {
       if (!no_xchg) {
         __syncthreads();
@@ -305,12 +343,12 @@ struct TeamFft {
     }
   }
 
-  template <int S, int DIR, int PAR>
+  template <int S, int DIR, int PAR, uint32_t ZM>
   static __device__ __forceinline__ void stages(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
                                                 bool no_xchg) {
     if constexpr (S < NST) {
-      stage<S, DIR, PAR>(d, lds, tw, t, no_xchg);
-      stages<S + 1, DIR, PAR>(d, lds, tw, t, no_xchg);
+      stage<S, DIR, PAR, ZM>(d, lds, tw, t, no_xchg);
+      stages<S + 1, DIR, PAR, ZM>(d, lds, tw, t, no_xchg);
     }
   }
 
@@ -325,14 +363,17 @@ struct TeamFft {
   // caller's antenna loop LICM would hoist all of them (~60 VGPRs) out of the loop and
   // spill.  Laundering t and tw through empty asm makes them opaque per transform:
   // they are re-derived (cheap ALU + L1-hit loads) instead of held.
-  template <int DIR, int PAR = 0>
+  //
+  // ZM: registers d[m] (bit m) that are zero in every thread on entry (the IFFT's
+  // out-of-band bins); stage 0 skips their additions.
+  template <int DIR, int PAR = 0, uint32_t ZM = 0>
   static __device__ __forceinline__ void run(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
                                              bool no_xchg = false) {
     const float2* twl = tw;
     int tl = t;
     asm volatile("" : "+s"(twl));
     asm volatile("" : "+v"(tl));
-    stages<0, DIR, PAR>(d, lds, twl, tl, no_xchg);
+    stages<0, DIR, PAR, ZM>(d, lds, twl, tl, no_xchg);
   }
   // IFFT then FFT of one antenna / CNC iteration: an even number of exchanges in total.
   template <int DIR>

@@ -92,6 +92,14 @@ struct Slots {
   static constexpr int P = F / T;
   static constexpr int HALF = NSLOT / 2;
   static constexpr int m_of(int s) { return ALIGNED ? (s < HALF ? s : P - NSLOT + s) : s; }
+  // Registers the scatter leaves zero in every thread: the out-of-band middle
+  // (HALF + 1 .. P - HALF - 1; register HALF holds thread 0's bin S/2).  Generic: none.
+  static constexpr uint32_t zero_mask() {
+    uint32_t m = 0;
+    if (ALIGNED)
+      for (int r = HALF + 1; r < P - HALF; ++r) m |= 1u << r;
+    return m;
+  }
 
   static __device__ __forceinline__ int k_of(int s, int t, int S, bool& valid) {
     if constexpr (ALIGNED) {
@@ -583,7 +591,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         if (lane == 0) vk_part[a & 1][wid] = vk;  // read after the IFFT's first barrier
       }
       SL::scatter(d, x, t0);
-      if (!MIMO_ABL(p, ABL_FFT)) FFT::template run<+1>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG));
+      if (!MIMO_ABL(p, ABL_FFT)) FFT::template run<+1, 0, SL::zero_mask()>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG));
       if (!MIMO_ABL(p, ABL_PA)) pa_block(p.pa_kind, d, p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
       if (!MIMO_ABL(p, ABL_FFT)) FFT::template run_second<-1>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG));
       if (MIMO_ABL(p, ABL_FFT)) __syncthreads();  // keep the vk_part hand-off ordered
@@ -699,7 +707,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       for (int s = 0; s < NSLOT; ++s)
         x[s] = ((valid_mask >> s) & 1u) ? cscale(qam_point(lh[s], L, hb), inv_sqrt_f) : make_float2(0.f, 0.f);
       SL::scatter(d, x, t0);
-      FFT::template run<+1>(d, lds, p.tw, t);
+      FFT::template run<+1, 0, SL::zero_mask()>(d, lds, p.tw, t);
       pa_block(p.cnc_pa_kind, d, p.sat_cnc, p.sqrt_sat_cnc, p.inv_sat_cnc, p.rapp_p, p.toi_cnc);
       FFT::template run_second<-1>(d, lds, p.tw, t);
       const float sc = inv_sqrt_f * p.inv_alpha_cnc;
