@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import argparse
 import os
+import time
 
 import numpy as np
 
@@ -179,7 +180,9 @@ def main():
     iters = np.asarray([int(x) for x in args.iters.split(",")])
     incl_clean = args.grid == "ber_vs_ebn0"
     link = _build_link(args, local)
+    t0 = time.perf_counter()
     err, bits = run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean, args.seed, rank, world, dist, local)
+    elapsed = time.perf_counter() - t0
     if rank == 0:
         ber = ber_from_counts(err, bits)
         tag = "%s_%s_nant%d" % (args.receiver, args.channel, args.n_ant)
@@ -196,7 +199,9 @@ def main():
                     tag, ibo, min(ebn0_arr), max(ebn0_arr), ebn0_arr[1] - ebn0_arr[0],
                     "_".join(str(v) for v in iters[1:]))
                 save_to_csv(ber_vs_ebn0_rows(ebn0_arr, ber[i].T), name, directory=args.out)
-        print(f"sweep done: {len(ibo_arr) * len(ebn0_arr)} points on {world} GPU(s) -> {args.out}")
+        n_sym = int(bits[..., 0].sum()) // (args.n_sc * int(np.log2(args.qam)))
+        print(f"sweep done: {len(ibo_arr) * len(ebn0_arr)} points, {n_sym} OFDM symbols on {world} GPU(s) in "
+              f"{elapsed:.1f} s -> {args.out}")
     if dist is not None:
         dist.destroy_process_group()
 
