@@ -3,8 +3,9 @@
 // One workgroup ("team", T threads) runs one trial = one OFDM symbol of
 // mp_model.Link.simulate (mp_model.py:180-222; clean run :133-175) entirely on chip:
 //
-//   labels (Philox BITS)                                  mp_model.py:208
-//   pass 1: channel draws -> MRT norms sum_a |H|^2         antenna_array.py:162-173
+//   labels (Philox BITS) -> pre-weighted symbols s / ||H|| / sqrt(F) (LDS)   mp_model.py:208
+//   pass 1: channel power draws -> MRT norms sum_a |H|^2   antenna_array.py:162-173
+//           (Rayleigh: rho^2 = -ln u1 only, no sqrt / sin / cos)
 //   pass 3: per antenna a
 //       H (Philox CHAN x FSPL, or closed-form LoS/two-path)  channel.py:35-72,116-167,262-275
 //       alpha_a from the per-antenna precoding power      mp_model.py:312-326
@@ -14,10 +15,15 @@
 //   CNC (corrector.py:52-112) or MCNC (corrector.py:165-207) iterations, hard slicer,
 //   XOR-popcount bit errors -> counts[trial][idx]         mp_model.py:215-222
 //
-// Nothing per trial touches HBM except the final per-trial counts (n_idx x 4 B): the
-// channel is regenerated from Philox instead of being stored.
-// Frequency-domain data live in the team FFT's cyclic register layout; each thread
-// owns NSLOT in-band sub-carriers ("slots").
+// Nothing per trial touches HBM except the final per-trial counts (n_idx x 4 B) and the
+// receiver stage's register spills: the channel is regenerated from Philox instead of
+// being stored.  Frequency-domain data live in the team FFT's cyclic
+// register layout; each thread owns NSLOT in-band sub-carriers ("slots").
+//
+// Without CSI errors the per-sub-carrier FSPL ratio f_c/f_k is factored out of the
+// antenna loops (it cancels in MRT) and the per-antenna ratio is folded into the
+// Box-Muller radius; alpha_a comes from a host-fitted polynomial (F <= 4096).  The
+// kernel is fp32-VALU-issue-bound.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
