@@ -111,3 +111,32 @@ def test_workers_share_counters_like_the_reference_drivers():
     ber, ber1 = e / b, np.asarray(err1[:]) / np.asarray(bits1[:])
     sig = np.sqrt(ber1 / b) * 4 + 1e-6
     assert np.all(np.abs(ber - ber1) < 6 * sig), (ber, ber1)
+
+
+def test_published_curve_paper_config():
+    """The whole published BER-vs-Eb/N0 curve of the paper config (64 ant, F 4096, 2048 sc,
+    64-QAM, IBO 3 dB, Rayleigh; figs/csv_results row layout: axis, no-distortion, standard
+    RX, CNC iterations 1..8) against the engine at 16,384 trials (2e8 bits) per point.
+    Compared where the published BER >= 1e-4 (the reference's own counts are small below
+    that): within 5 % relative (measured: <= 2.6 %, most points < 0.6 %)."""
+    import os
+    import utilities
+    from gpu_util import engine_for
+    from oracle import sim
+    d = os.path.join(os.path.dirname(__file__), "golden")
+    rows = np.asarray(utilities.read_from_csv("published_ber_vs_ebn0_cnc_rayleigh_ibo3", directory=d))
+    ebn0 = rows[0]
+    checked = 0
+    for j, e in enumerate(ebn0):
+        snr = float(sim.rm.ebn0_to_snr(e, 2048, 2048, 64))
+        cfg = sim.SimConfig(64, 2048, 4096, 64, pa="softlim", ibo_db=3.0, snr_db=snr)
+        eng = engine_for(cfg)
+        err, bits, _ = eng.run(4242 + j, 0, 16384, [0, 1, 2, 3, 4], True)
+        ber = err / bits
+        pub = rows[1:7, j]
+        sel = pub >= 1e-4
+        checked += int(sel.sum())
+        rel = np.abs(ber[sel] - pub[sel]) / pub[sel]
+        print(e, ber, pub, rel)
+        assert np.all(rel < 0.05), (e, ber, pub)
+    assert checked >= 40
