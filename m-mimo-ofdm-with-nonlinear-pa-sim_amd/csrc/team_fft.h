@@ -29,6 +29,9 @@
 #ifndef MIMO_TW_LOAD_MAX
 #define MIMO_TW_LOAD_MAX 64  // twiddle powers r <= this are loaded (1: square the rest; measured neutral)
 #endif
+#ifndef MIMO_PADN_SHIFT
+#define MIMO_PADN_SHIFT 5  // padding of exchanges >= 1
+#endif
 #ifndef MIMO_PAD0_SHIFT
 #define MIMO_PAD0_SHIFT 4
 #endif
@@ -197,8 +200,9 @@ struct TeamFft {
   // Padding of exchange S: one slot per 2^PSH elements.  Exchange 0 (stage 0 writes
   // 16t + r) uses 1/16 (MIMO_PAD0_SHIFT): it halves that exchange's modelled bank
   // conflicts (tools/lds_conflicts.py); later exchanges use 1/32.
-  static constexpr int psh(int S) { return S == 0 ? MIMO_PAD0_SHIFT : 5; }
-  static constexpr int LDS_ELEMS = F + F / (1 << (MIMO_PAD0_SHIFT < 5 ? MIMO_PAD0_SHIFT : 5));
+  static constexpr int psh(int S) { return S == 0 ? MIMO_PAD0_SHIFT : MIMO_PADN_SHIFT; }
+  static constexpr int LDS_ELEMS =
+      F + F / (1 << (MIMO_PAD0_SHIFT < MIMO_PADN_SHIFT ? MIMO_PAD0_SHIFT : MIMO_PADN_SHIFT));
   static_assert((1 << LOG_F) == F && (1 << LOG_P) == P && P >= 2, "power-of-two sizes");
 
   static constexpr int bits(int s) { return fft_bits(F, P, s); }
