@@ -23,14 +23,19 @@ CASES = [
     (1024, 1000, 8, 16, "softlim", 0.0, 1.0, None),  # generic slots (S % 4T != 0)
     (512, 256, 16, 4, "toi", 0.0, 5.0, None),        # QPSK, cubic PA
     (2048, 1024, 8, 256, "softlim", 0.0, 0.0, None),  # 256-QAM at IBO 0 (strong clipping)
+    (128, 4, 2, 16, "softlim", 0.0, -2.0, None),     # smallest band (4 sub-carriers), deep clipping
+    (256, 252, 4, 16, "softlim", 0.0, 2.0, None),    # widest band allowed (S = F - 4)
+    (256, 128, 2048, 64, "softlim", 0.0, 0.0, None),  # many antennas
+    (1024, 512, 1, 1024, "softlim", 0.0, 100.0, None),  # SISO, ideal PA, 1024-QAM
 ]
+EBN0 = {(128, 4): 6.0, (256, 128): 8.0, (1024, 512): 30.0}
 
 
 @pytest.mark.parametrize("F,S,A,M,pa,p,ibo,team", CASES)
 def test_sizes_vs_oracle(monkeypatch, F, S, A, M, pa, p, ibo, team):
     if team is not None:
         monkeypatch.setenv("MIMO_TEAM", str(team))
-    snr = float(sim.rm.ebn0_to_snr(14.0, S, S, M))
+    snr = float(sim.rm.ebn0_to_snr(EBN0.get((F, S), 14.0), S, S, M))
     cfg = sim.SimConfig(A, S, F, M, pa=pa, p_hardness=p, ibo_db=ibo, snr_db=snr)
     trials = np.arange(24)
     iters = [0, 1, 2]
