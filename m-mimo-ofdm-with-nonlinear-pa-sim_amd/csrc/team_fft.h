@@ -10,8 +10,8 @@
 // registers.  The last stage writes j + r*F/R as well, so input and output are both
 // cyclic and a transform needs (stages - 1) exchanges through padded LDS buffers
 // (one pad slot per 32 elements: conflict-free ds_write_b64 / ds_read_b64 for the
-// stage patterns used here).  F = 2048 with P = 16 is radix 16 x 16 x 8: two
-// exchanges, two barriers.
+// stage patterns used here).  F = 2048 with P = 16 is radix 16 x 8 x 16 (plan below): two
+// exchanges.
 //
 // Two alternating exchange buffers: one barrier per exchange (see stage()).
 //
@@ -61,7 +61,19 @@ constexpr int ilog2(int n) { return n <= 1 ? 0 : 1 + ilog2(n >> 1); }
 // jm < NS, 1 <= r < R, stored per stage as a [R][NS] block (lane-contiguous in jm) of
 // one table; fft_tw_off(s) is the block's offset.
 constexpr int fft_nst(int F, int P) { return (ilog2(F) + ilog2(P) - 1) / ilog2(P); }
+// Radix plan.  MIMO_FFT_PLAN 1: the last stage has radix P (one butterfly per thread,
+// NS = T), the other bits are spread front-loaded over the earlier stages.  Every stage
+// then has NS <= T, so the twiddles of a thread's butterflies i > 0 equal those of
+// butterfly 0 (no compile-time rotations), e.g. F = 2048, P = 16: 16 x 8 x 16.
+// Plan 0: front-loaded (16 x 16 x 8; the last stage's second butterfly rotates).
+#ifndef MIMO_FFT_PLAN
+#define MIMO_FFT_PLAN 1
+#endif
 constexpr int fft_bits(int F, int P, int s) {
+  if (MIMO_FFT_PLAN == 1 && fft_nst(F, P) > 1) {
+    const int n = fft_nst(F, P) - 1, rest = ilog2(F) - ilog2(P);
+    return s == n ? ilog2(P) : rest / n + (s < rest % n ? 1 : 0);
+  }
   return ilog2(F) / fft_nst(F, P) + (s < ilog2(F) % fft_nst(F, P) ? 1 : 0);
 }
 constexpr int fft_bits_before(int F, int P, int s) { return s == 0 ? 0 : fft_bits_before(F, P, s - 1) + fft_bits(F, P, s - 1); }

@@ -33,7 +33,7 @@ struct Profile {
 };
 constexpr Profile profile_for(int T, bool aligned, int ch) {
   const int P = kF / T;
-  if (!aligned) return Profile{2, kF >= 8192 ? 1 : 2, true};
+  if (!aligned) return Profile{2, kF >= 4096 ? 1 : 2, true};  // one buffer from F = 4096: 2 teams/CU
   if (ch == CH_TWOPATH && MIMO_TWOPATH_W2) return Profile{2, 2, false};  // fp64 geometry: register-heavy
   if (P < 16) return Profile{4, 2, false};
   if (kF <= 4096) return Profile{MIMO_MINW16, MIMO_MINW16 == 3 ? 1 : 2, MIMO_MINW16 == 3};

@@ -8,12 +8,18 @@ on one bank.  Prints extra cycles per transform for candidate layouts.
 import itertools
 import sys
 
+PLAN = 1  # team_fft.h MIMO_FFT_PLAN
+
 
 def stages(F, T):
     P = F // T
     lf, lp = F.bit_length() - 1, P.bit_length() - 1
     nst = (lf + lp - 1) // lp
-    bits = [lf // nst + (1 if s < lf % nst else 0) for s in range(nst)]
+    if PLAN == 1 and nst > 1:  # team_fft.h MIMO_FFT_PLAN 1: radix P last, the rest front-loaded
+        n, rest = nst - 1, lf - lp
+        bits = [rest // n + (1 if s < rest % n else 0) for s in range(n)] + [lp]
+    else:
+        bits = [lf // nst + (1 if s < lf % nst else 0) for s in range(nst)]
     out, ns = [], 1
     for b in bits:
         out.append((1 << b, ns))
