@@ -48,6 +48,9 @@ constexpr int kMaxCsiAnt = 512;  // CSI-error runs: antennas (LDS per team; engi
 #ifndef MIMO_ALPHA_POLY
 #define MIMO_ALPHA_POLY 1
 #endif
+#ifndef MIMO_VK_DPP
+#define MIMO_VK_DPP 1  // per-antenna precoding-power wave sum by DPP (0: __shfl_xor)
+#endif
 
 struct TrialParams {
   uint64_t seed;
@@ -162,15 +165,34 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Wave sum delivered in lane 63 only (other lanes hold partial sums): DPP adds on the
+// VALU instead of the six dependent ds_bpermute round trips of __shfl_xor.  Per row of
+// 16 lanes: pair / quad swaps and the half-row / row mirrors give every lane its row sum;
+// row_bcast:15 then row_bcast:31 fold rows 0-2 into row 3.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_add(float v) {
+  const int s = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, false);
+  return v + __builtin_bit_cast(float, s);
+}
+__device__ __forceinline__ float wave_sum_lane63(float v) {
+  v = dpp_add<0xB1>(v);        // quad_perm [1,0,3,2]
+  v = dpp_add<0x4E>(v);        // quad_perm [2,3,0,1]
+  v = dpp_add<0x141>(v);       // row_half_mirror
+  v = dpp_add<0x140>(v);       // row_mirror
+  v = dpp_add<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3
+  v = dpp_add<0x143, 0xC>(v);  // row_bcast:31 into rows 2 and 3
+  return v;
+}
+
 // Team-wide sum; every thread gets the result.  Two barriers.
 template <int T>
 __device__ __forceinline__ float team_sum(float v, float* red) {
-  v = wave_sum(v);
   if constexpr (T == 64) {
-    return v;
+    return wave_sum(v);
   } else {
+    v = wave_sum_lane63(v);
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    if ((threadIdx.x & 63) == 63) red[threadIdx.x >> 6] = v;
     __syncthreads();
     float s = 0.f;
 #pragma unroll
@@ -593,8 +615,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         vk = fmaf(e2[s], inv_nrm[s] * inv_nrm[s], vk);  // inv_nrm = 0 off band
       }
       if (main_pass) {
+#if MIMO_VK_DPP
+        vk = wave_sum_lane63(vk);
+        if (lane == 63) vk_part[a & 1][wid] = vk;  // read after the IFFT's first barrier
+#else
         vk = wave_sum(vk);
-        if (lane == 0) vk_part[a & 1][wid] = vk;  // read after the IFFT's first barrier
+        if (lane == 0) vk_part[a & 1][wid] = vk;
+#endif
       }
       SL::scatter(d, x, t0);
       if (!MIMO_ABL(p, ABL_FFT)) FFT::template run<+1, 0, SL::zero_mask()>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG));
