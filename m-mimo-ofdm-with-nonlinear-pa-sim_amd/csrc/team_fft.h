@@ -29,6 +29,9 @@
 #ifndef MIMO_TW_LOAD_MAX
 #define MIMO_TW_LOAD_MAX 64  // twiddle powers r <= this are loaded (1: square the rest; measured neutral)
 #endif
+#ifndef MIMO_TW_PREFETCH
+#define MIMO_TW_PREFETCH 1  // load every stage's base twiddles at the start of a transform (F <= 4096)
+#endif
 #ifndef MIMO_PADN_SHIFT
 #define MIMO_PADN_SHIFT 5  // padding of exchanges >= 1
 #endif
@@ -318,9 +321,35 @@ struct TeamFft {
   // VGPR offset); the other r are products w(jm, a) w(jm, b), a + b = r (at most
   // log2 R - 1 roundings).  Loads, not multiplies, were the twiddles' cost: dropping the
   // loads saved 17 % of the kernel, dropping the multiplies 8 % (profiles/r01).
+  // Base twiddles w(jm0, 2^b) of every stage >= 1, loaded together at the start of a
+  // transform (MIMO_TW_PREFETCH): their L2 latency then overlaps stage 0 and the first
+  // exchange instead of stalling each stage's first twiddle multiply.
+  static constexpr int kMaxB = 5;
+  // Measured -1.1 % (F 2048), -1.5 % (F 4096), +0.9 % (F 8192: more stages held live).
+  static constexpr bool PREFETCH = MIMO_TW_PREFETCH && F <= 4096;
+  struct Base {
+    float2 v[NST][kMaxB];
+  };
+  template <int S>
+  static __device__ __forceinline__ void load_base(Base& b, const float2* __restrict__ tw, int t) {
+    if constexpr (S < NST) {
+      constexpr int R = 1 << bits(S);
+      constexpr int NS = 1 << bits_before(S);
+      if constexpr (NS > 1) {
+        constexpr int TW_OFF = fft_tw_off(F, P, S);
+        const int jm0 = t & (NS - 1);
+#pragma unroll
+        for (int k = 0; k < bits(S) && k < kMaxB && (1 << k) <= MIMO_TW_LOAD_MAX; ++k)
+          b.v[S][k] = gload(tw + TW_OFF + (1 << k) * NS, jm0);
+        (void)R;
+      }
+      load_base<S + 1>(b, tw, t);
+    }
+  }
+
   template <int S, int DIR, int PAR, uint32_t ZM>
   static __device__ __forceinline__ void stage(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
-                                               bool no_xchg) {
+                                               bool no_xchg, const Base& base) {
     constexpr int R = 1 << bits(S);
     constexpr int NS = 1 << bits_before(S);
     constexpr int B = P / R;
@@ -328,7 +357,18 @@ struct TeamFft {
     static_assert(B >= 1 && B * R == P, "radix must divide points per thread");
     float2* buf = lds + (NBUF == 2 ? ((S + PAR) & 1) * LDS_ELEMS : 0);
     float2 w0[R];
-    if constexpr (NS > 1) {
+    if constexpr (NS > 1 && PREFETCH) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        if ((r & (r - 1)) == 0) {
+          w0[r] = r <= MIMO_TW_LOAD_MAX ? base.v[S][ilog2(r)] : cmul(w0[r / 2], w0[r / 2]);
+        } else {
+          int hb = r;
+          while (hb & (hb - 1)) hb &= hb - 1;
+          w0[r] = cmul(w0[hb], w0[r - hb]);
+        }
+      }
+    } else if constexpr (NS > 1) {
       constexpr int TW_OFF = fft_tw_off(F, P, S);  // forced compile-time (a runtime call otherwise)
       const float2* tws = tw + TW_OFF;
       const int jm0 = t & (NS - 1);
@@ -361,10 +401,10 @@ struct TeamFft {
 
   template <int S, int DIR, int PAR, uint32_t ZM>
   static __device__ __forceinline__ void stages(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
-                                                bool no_xchg) {
+                                                bool no_xchg, const Base& base) {
     if constexpr (S < NST) {
-      stage<S, DIR, PAR, ZM>(d, lds, tw, t, no_xchg);
-      stages<S + 1, DIR, PAR, ZM>(d, lds, tw, t, no_xchg);
+      stage<S, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base);
+      stages<S + 1, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base);
     }
   }
 
@@ -389,7 +429,9 @@ struct TeamFft {
     int tl = t;
     asm volatile("" : "+s"(twl));
     asm volatile("" : "+v"(tl));
-    stages<0, DIR, PAR, ZM>(d, lds, twl, tl, no_xchg);
+    Base base;
+    if constexpr (PREFETCH) load_base<1>(base, twl, tl);
+    stages<0, DIR, PAR, ZM>(d, lds, twl, tl, no_xchg, base);
   }
   // IFFT then FFT of one antenna / CNC iteration: an even number of exchanges in total.
   template <int DIR>
