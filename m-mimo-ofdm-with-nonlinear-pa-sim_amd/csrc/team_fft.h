@@ -347,9 +347,9 @@ struct TeamFft {
     }
   }
 
-  template <int S, int DIR, int PAR, uint32_t ZM>
+  template <int S, int DIR, int PAR, uint32_t ZM, typename Fill>
   static __device__ __forceinline__ void stage(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
-                                               bool no_xchg, const Base& base) {
+                                               bool no_xchg, const Base& base, const Fill& fill) {
     constexpr int R = 1 << bits(S);
     constexpr int NS = 1 << bits_before(S);
     constexpr int B = P / R;
@@ -396,15 +396,18 @@ struct TeamFft {
 #pragma unroll
         for (int m = 0; m < P; ++m) d[m] = rb[pad<S>(T * m)];
       }
+      // Independent caller work placed between this exchange's reads and their first use
+      // (same basic block: the scheduler interleaves it with the LDS latency).
+      fill(S);
     }
   }
 
-  template <int S, int DIR, int PAR, uint32_t ZM>
+  template <int S, int DIR, int PAR, uint32_t ZM, typename Fill>
   static __device__ __forceinline__ void stages(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
-                                                bool no_xchg, const Base& base) {
+                                                bool no_xchg, const Base& base, const Fill& fill) {
     if constexpr (S < NST) {
-      stage<S, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base);
-      stages<S + 1, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base);
+      stage<S, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base, fill);
+      stages<S + 1, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base, fill);
     }
   }
 
@@ -422,22 +425,25 @@ struct TeamFft {
   //
   // ZM: registers d[m] (bit m) that are zero in every thread on entry (the IFFT's
   // out-of-band bins); stage 0 skips their additions.
-  template <int DIR, int PAR = 0, uint32_t ZM = 0>
+  struct NoFill {
+    __device__ __forceinline__ void operator()(int) const {}
+  };
+  template <int DIR, int PAR = 0, uint32_t ZM = 0, typename Fill = NoFill>
   static __device__ __forceinline__ void run(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
-                                             bool no_xchg = false) {
+                                             bool no_xchg = false, const Fill& fill = Fill{}) {
     const float2* twl = tw;
     int tl = t;
     asm volatile("" : "+s"(twl));
     asm volatile("" : "+v"(tl));
     Base base;
     if constexpr (PREFETCH) load_base<1>(base, twl, tl);
-    stages<0, DIR, PAR, ZM>(d, lds, twl, tl, no_xchg, base);
+    stages<0, DIR, PAR, ZM>(d, lds, twl, tl, no_xchg, base, fill);
   }
   // IFFT then FFT of one antenna / CNC iteration: an even number of exchanges in total.
-  template <int DIR>
+  template <int DIR, typename Fill = NoFill>
   static __device__ __forceinline__ void run_second(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
-                                                    bool no_xchg = false) {
-    run<DIR, XCHG & 1>(d, lds, tw, t, no_xchg);
+                                                    bool no_xchg = false, const Fill& fill = Fill{}) {
+    run<DIR, XCHG & 1, 0u, Fill>(d, lds, tw, t, no_xchg, fill);
   }
 };
 

@@ -48,6 +48,9 @@ constexpr int kMaxCsiAnt = 512;  // CSI-error runs: antennas (LDS per team; engi
 #ifndef MIMO_ALPHA_POLY
 #define MIMO_ALPHA_POLY 1
 #endif
+#ifndef MIMO_HPIPE
+#define MIMO_HPIPE 1  // draw antenna a+1's channel inside antenna a's FFT exchanges (aligned Rayleigh)
+#endif
 #ifndef MIMO_VK_DPP
 #define MIMO_VK_DPP 1  // per-antenna precoding-power wave sum by DPP (0: __shfl_xor)
 #endif
@@ -336,6 +339,30 @@ struct Channel {
     }
   }
 
+  // One Philox call's worth of normals() (aligned instances): chunk c = 2 j + band fills
+  // slots (j, j + Q) of the positive band (band 0) or (HALF + j, HALF + j + Q) of the
+  // negative band (band 1).  normals() == all 2 Q chunks.
+  static constexpr int kChunks = ALIGNED ? SL::HALF : 0;
+  static __device__ __forceinline__ void normals_chunk(int c, Key key, uint32_t trial, uint32_t stream, uint32_t aux,
+                                                       int t, int S, float2 (&z)[NSLOT], float cs) {
+    if constexpr (ALIGNED) {
+      constexpr int Q = SL::HALF / 2;
+      const int j = c >> 1;
+      float2 z1, z2;
+      if ((c & 1) == 0) {
+        const bool sw = (j == 0) && (t == 0);
+        cn_pair(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)((S >> 2) - 1 + t + T * j), trial, stream, aux, z1, z2,
+                cs);
+        z[j] = sw ? z2 : z1;
+        z[j + Q] = sw ? z1 : z2;
+      } else {
+        cn_pair(key, (uint32_t)(t + T * j), trial, stream, aux, z1, z2, cs);
+        z[SL::HALF + j] = z1;
+        z[SL::HALF + j + Q] = z2;
+      }
+    }
+  }
+
   // |H|^2 of antenna a at the thread's slots (Rayleigh, FSPL factor f_rel left out as in
   // gen<false>): the same draws as gen(), magnitudes only.
   static __device__ __forceinline__ void power(const TrialParams& p, Key key, uint32_t trial, int a, int t,
@@ -588,10 +615,41 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   auto array_pass = [&](bool main_pass, float2 (&acc)[NSLOT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) acc[s] = make_float2(0.f, 0.f);
+    // Software pipeline (PIPE): antenna a+1's channel draws (one Philox call per chunk)
+    // run inside antenna a's FFT exchanges, where the wave otherwise waits on LDS.
+    constexpr bool PIPE = MIMO_HPIPE && ALIGNED && CH == CH_RAYLEIGH && !CSI;
+    float2 hnext[PIPE ? NSLOT : 1];
+    if constexpr (PIPE) {
+      const float sa = p.ant_rel[0];
+      if (MIMO_ABL(p, ABL_RNG)) CHN::template gen<FREL>(p, key, trial, 0, t, rx, hnext);
+      else CHN::normals(key, trial, ST_CHAN, 0u, t, S, hnext, kNegLn2 * (sa * sa));
+    }
     for (int a = 0; a < A; ++a) {
       const int tl = opaque(t);
       float2 h[NSLOT];
-      CHN::template gen<FREL>(p, key, trial, a, tl, rx, h);
+      if constexpr (PIPE) {
+#pragma unroll
+        for (int s = 0; s < NSLOT; ++s) h[s] = hnext[s];
+      } else {
+        CHN::template gen<FREL>(p, key, trial, a, tl, rx, h);
+      }
+      const int an = a + 1 < A ? a + 1 : a;  // the last antenna redraws itself (unused)
+      const float san = PIPE ? p.ant_rel[an] : 0.f;
+      // Window w of NW = 2 XCHG exchange windows (IFFT then FFT) draws chunks
+      // [w NC / NW, (w + 1) NC / NW) of antenna a+1.
+      auto hfill = [&](int w) __attribute__((always_inline)) {
+        if constexpr (PIPE) {
+          constexpr int NC = CHN::kChunks, NW = 2 * FFT::XCHG;
+          if (!MIMO_ABL(p, ABL_RNG)) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+              if (c >= w * NC / NW && c < (w + 1) * NC / NW)
+                CHN::normals_chunk(c, key, trial, ST_CHAN, (uint32_t)an, tl, S, hnext, kNegLn2 * (san * san));
+          }
+        }
+      };
+      auto hfill_ifft = [&](int w) __attribute__((always_inline)) { hfill(w); };
+      auto hfill_fft = [&](int w) __attribute__((always_inline)) { hfill(FFT::XCHG + w); };
       float2 he[CSI ? NSLOT : 1];
       if constexpr (CSI) {
         float2 zc[NSLOT];
@@ -624,9 +682,16 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 #endif
       }
       SL::scatter(d, x, t0);
-      if (!MIMO_ABL(p, ABL_FFT)) FFT::template run<+1, 0, SL::zero_mask()>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG));
+      if (!MIMO_ABL(p, ABL_FFT))
+        FFT::template run<+1, 0, SL::zero_mask()>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_ifft);
       if (!MIMO_ABL(p, ABL_PA)) pa_block(p.pa_kind, d, p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
-      if (!MIMO_ABL(p, ABL_FFT)) FFT::template run_second<-1>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG));
+      if (!MIMO_ABL(p, ABL_FFT)) FFT::template run_second<-1>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_fft);
+      if constexpr (PIPE) {
+        if (MIMO_ABL(p, ABL_FFT) || MIMO_ABL(p, ABL_XCHG)) {  // no exchange windows ran
+#pragma unroll
+          for (int w = 0; w < 2 * FFT::XCHG; ++w) hfill(w);
+        }
+      }
       if (MIMO_ABL(p, ABL_FFT)) __syncthreads();  // keep the vk_part hand-off ordered
       float alpha_a = 0.f;
       if (main_pass) {
