@@ -63,9 +63,12 @@ def bytes_alg_per_trial(a=A, s=S, f=F):
     return 8 * a * (6 * s + 2 * f)
 
 
-def flops_alg_per_trial(a=A, s=S, f=F):
-    """A (2 * 5 F log2 F + 14 S + 12 F)  (FFT pair + precode/PA/combine)."""
-    return a * (10 * f * np.log2(f) + 14 * s + 12 * f)
+def flops_alg_per_trial(a=A, s=S, f=F, max_iter=0, mcnc=False):
+    """A (2 * 5 F log2 F + 14 S + 12 F)  (FFT pair + precode/PA/combine), plus
+    per receiver iteration one single-vector IFFT/PA/FFT (CNC, corrector.py:84-110) or one
+    more array pass (MCNC, corrector.py:165-207)."""
+    one = 10 * f * np.log2(f) + 14 * s + 12 * f
+    return a * one + max_iter * (a * one if mcnc else one)
 
 
 def make_engine(device, workload="2"):
@@ -104,24 +107,27 @@ def make_engine(device, workload="2"):
     return link.engine()
 
 
-def cpu_baseline(seconds=15.0, workload="2"):
+def cpu_baseline(seconds=15.0, workload="2", iters=(0,)):
     """The float64 oracle (oracle/sim.py, NumPy, one process / one core) on a bounded sample
-    of the same workload: reported beside the GPU number, never the measured product."""
+    of the same workload (same receiver iterations): reported beside the GPU number, never
+    the measured product."""
     from oracle import refmath as rm
     from oracle.sim import SimConfig, run_trials
     w = WORKLOADS[workload]
     cfg = SimConfig(w["A"], w["S"], w["F"], w["M"], pa=w["pa"], p_hardness=w["p"], ibo_db=w["ibo"],
                     snr_db=float(rm.ebn0_to_snr(w["ebn0"], w["S"], w["S"], w["M"])), channel=w.get("chan", "rayleigh"),
                     receiver="mcnc" if w.get("mcnc") else "cnc", csi_eps=w.get("csi"))
-    run_trials(cfg, 7, [0], iters=[0])  # warm caches / imports
+    iters = list(iters)
+    run_trials(cfg, 7, [0], iters=iters)  # warm caches / imports
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         step = 16 if w["F"] <= 2048 else 2
-        run_trials(cfg, 7, np.arange(n, n + step), iters=[0])
+        run_trials(cfg, 7, np.arange(n, n + step), iters=iters)
         n += step
     dt = time.perf_counter() - t0
+    rx = "standard RX" if iters == [0] else f"receiver iterations {iters}"
     return dict(value=round(n / dt, 3), unit="OFDM symbols/s", cores=1, kind="port",
-                sample=f"{n} trials of the workload-{workload} chain (standard RX) through oracle/sim.py "
+                sample=f"{n} trials of the workload-{workload} chain ({rx}) through oracle/sim.py "
                        f"(NumPy float64, 1 process, {dt:.1f} s)")
 
 
@@ -203,7 +209,8 @@ def main():
     value = total_trials / dt
     avg_kernel_s = kern_ms / 1e3 / args.steps
     b_alg = bytes_alg_per_trial(wl["A"], wl["S"], wl["F"]) * B
-    f_alg = flops_alg_per_trial(wl["A"], wl["S"], wl["F"]) * B
+    f_trial = flops_alg_per_trial(wl["A"], wl["S"], wl["F"], max(iters), wl.get("mcnc", False))
+    f_alg = f_trial * B
     traffic, traffic_src = load_pmc_traffic(B) if args.workload == "2" else (None, None)
     out = {
         "metric": "OFDM symbols/s/GPU (64-ant,1024-sc) + achieved HBM %peak; BER match vs ref",
@@ -226,7 +233,7 @@ def main():
             "frac": round(f_alg / avg_kernel_s / 1e12 / FP32_PEAK_TFLOPS, 4),
             "traffic": traffic, "traffic_source": traffic_src,
             "kernel": "mimo::trial_kernel " + eng.describe(), "kernel_ms": round(avg_kernel_s * 1e3, 3),
-            "flops_alg_per_trial": flops_alg_per_trial(wl["A"], wl["S"], wl["F"]),
+            "flops_alg_per_trial": f_trial,
         },
         "hbm_alg": {"achieved": round(b_alg / avg_kernel_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(b_alg / avg_kernel_s / 1e9 / HBM_PEAK_GBS, 4),
@@ -235,7 +242,7 @@ def main():
         "ber": [round(float(x) / (total_trials * wl["S"] * np.log2(wl["M"])), 8) for x in err_tot],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.workload)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.workload, iters)
     if dist:
         dist.destroy_process_group()
     if rank == 0:
