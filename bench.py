@@ -71,7 +71,7 @@ def flops_alg_per_trial(a=A, s=S, f=F, max_iter=0, mcnc=False):
     return a * one + max_iter * (a * one if mcnc else one)
 
 
-def make_engine(device, workload="2"):
+def make_engine(device, workload="2", precision="f64"):
     import _engine
     import mp_model  # noqa: F401  (host mirror; computes the per-point scalars like Link)
     from utilities import ebn0_to_snr
@@ -101,7 +101,7 @@ def make_engine(device, workload="2"):
         ch.calc_channel_mat(tx_transceivers=arr.array_elements, rx_transceiver=rx, skip_attenuation=False)
     link = mp_model.Link(mod_obj=mod, array_obj=arr, std_rx_obj=rx, chan_obj=ch, noise_obj=noise.Awgn(snr_db=10),
                          rx_loc_var=10.0, n_err_min=10 ** 12, bits_sent_max=10 ** 15, is_mcnc=w.get("mcnc", False),
-                         csi_epsylon=w.get("csi"), device=device)
+                         csi_epsylon=w.get("csi"), device=device, precision=precision)
     link.update_distortion(ibo_val_db=w["ibo"])
     link.set_snr(ebn0_to_snr(w["ebn0"], S, S, M))
     return link.engine()
@@ -153,6 +153,8 @@ def main():
     ap.add_argument("--iters", type=str, default="0", help="receiver iterations, e.g. 0 or 0,1,2,3,4")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--precision", default="f64", choices=["f64", "f32"],
+                    help="arithmetic type of the fused kernel (f64 = the reference's float64)")
     ap.add_argument("--workload", default="2", choices=sorted(WORKLOADS),
                     help="2 = BASELINE config 2 (headline); paper; 5su (config-5 array, one user)")
     args = ap.parse_args()
@@ -172,7 +174,7 @@ def main():
         torch.cuda.set_device(dev)
         dist.init_process_group(backend)
     wl = WORKLOADS[args.workload]
-    eng = make_engine(dev, args.workload)
+    eng = make_engine(dev, args.workload, args.precision)
     iters = [int(x) for x in args.iters.split(",")]
     B = args.batch
     seed = 2137
@@ -223,7 +225,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": args.precision,
         "data": "synthetic (on-device Philox bits / Rayleigh channel / AWGN)",
         "config": {"workload": wl["desc"] + (", standard RX" if iters == [0] else f", CNC iterations {iters}"),
                    "trials_per_gpu_per_step": B, "iters": iters, "parallelism": f"trial-sharded x{world}"},

@@ -37,12 +37,13 @@
 extern "C" {
 #endif
 
-#define MIMO_ABI_VERSION 1
+#define MIMO_ABI_VERSION 2
 
 enum { MIMO_OK = 0, MIMO_EINVAL = -1, MIMO_EHIP = -2, MIMO_ENOKERNEL = -3, MIMO_ENOMEM = -4 };
 enum { MIMO_PA_NONE = 0, MIMO_PA_SOFTLIM = 1, MIMO_PA_RAPP = 2, MIMO_PA_TOI = 3 };
 enum { MIMO_CH_RAYLEIGH = 1, MIMO_CH_LOS = 2, MIMO_CH_TWOPATH = 3 };
 enum { MIMO_RX_CNC = 1, MIMO_RX_MCNC = 2 };
+enum { MIMO_PREC_F64 = 0, MIMO_PREC_F32 = 1 };
 
 typedef struct mimo_engine mimo_engine;
 
@@ -59,7 +60,8 @@ typedef struct mimo_config {
   double rx_pos[3];         /* nominal RX position [m]                               */
   double rx_loc_var;        /* LoS / two-path RX jitter span [m] (mp_model.py:192-199) */
   int32_t reroll_chan;      /* 1: per-trial channel reroll (Link.simulate reroll_chan) */
-  int32_t reserved;
+  int32_t precision;        /* MIMO_PREC_F64 (0, default: the reference's complex128 /
+                               float64, modulation.py:270) or MIMO_PREC_F32 (fast variant) */
   const double* tx_pos;     /* [n_ant][3] antenna positions [m]                      */
   const double* carrier_freqs; /* [n_fft] carrier frequencies [Hz] in FFT-bin order  */
 } mimo_config;

@@ -17,6 +17,16 @@ LIB_PATH = os.environ.get("MIMO_LIB") or os.path.join(_HERE, "libmimo_engine.so"
 PA_KINDS = {"none": 0, "softlim": 1, "rapp": 2, "toi": 3}
 CH_KINDS = {"rayleigh": 1, "los": 2, "two_path": 3}
 RX_KINDS = {"cnc": 1, "mcnc": 2}
+# Arithmetic type of the fused kernel: "f64" is the reference's own precision (complex128 /
+# float64, the default); "f32" is the fast variant.  MIMO_PRECISION overrides the default.
+PRECISIONS = {"f64": 0, "f32": 1}
+
+
+def default_precision():
+    p = os.environ.get("MIMO_PRECISION", "f64").lower()
+    if p not in PRECISIONS:
+        raise ValueError(f"MIMO_PRECISION must be one of {sorted(PRECISIONS)}")
+    return p
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _i32p = ctypes.POINTER(ctypes.c_int32)
@@ -29,7 +39,7 @@ class MimoConfig(ctypes.Structure):
     _fields_ = [("n_ant", ctypes.c_int32), ("n_sub_carr", ctypes.c_int32), ("n_fft", ctypes.c_int32),
                 ("constel_size", ctypes.c_int32), ("cp_len", ctypes.c_int32), ("channel_kind", ctypes.c_int32),
                 ("receiver_kind", ctypes.c_int32), ("device", ctypes.c_int32), ("rx_pos", ctypes.c_double * 3),
-                ("rx_loc_var", ctypes.c_double), ("reroll_chan", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("rx_loc_var", ctypes.c_double), ("reroll_chan", ctypes.c_int32), ("precision", ctypes.c_int32),
                 ("tx_pos", _dp), ("carrier_freqs", _dp)]
 
 
@@ -113,15 +123,19 @@ class Engine:
     """One configured system (the deep-copied objects of a ``Link``) on one GPU."""
 
     def __init__(self, n_ant, n_sub_carr, n_fft, constel_size, cp_len, channel, receiver, tx_pos, rx_pos,
-                 rx_loc_var, carrier_freqs, reroll=True, device=-1):
+                 rx_loc_var, carrier_freqs, reroll=True, device=-1, precision=None):
         L = lib()
+        self.precision = precision or default_precision()
+        if self.precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
         self._tx = _c(tx_pos, np.float64).reshape(-1, 3)
         self._fr = _c(carrier_freqs, np.float64)
         if self._tx.shape[0] != n_ant or self._fr.shape[0] != n_fft:
             raise ValueError("tx_pos must be [n_ant, 3] and carrier_freqs [n_fft]")
         cfg = MimoConfig(n_ant=n_ant, n_sub_carr=n_sub_carr, n_fft=n_fft, constel_size=constel_size, cp_len=cp_len,
                          channel_kind=CH_KINDS[channel], receiver_kind=RX_KINDS[receiver], device=device,
-                         rx_loc_var=float(rx_loc_var), reroll_chan=int(bool(reroll)), reserved=0,
+                         rx_loc_var=float(rx_loc_var), reroll_chan=int(bool(reroll)),
+                         precision=PRECISIONS[self.precision],
                          tx_pos=_ptr(self._tx, ctypes.c_double), carrier_freqs=_ptr(self._fr, ctypes.c_double))
         cfg.rx_pos[:] = [float(v) for v in rx_pos]
         h = L.mimo_engine_create(ctypes.byref(cfg))

@@ -60,7 +60,8 @@ double alpha_exact(double g2) {
 // at 64 nodes, converted to monomials in x for a Horner evaluation in fp32.  Max relative
 // error ~1e-7 for IBO in [-10, 30] dB (fp32 rounding level); the kernel falls back to
 // the exact formula outside the interval.
-void fit_alpha(double g0sq, mimo::TrialParams& p) {
+template <typename P>
+void fit_alpha(double g0sq, P& p) {
   constexpr int N = 64, D = 8;
   constexpr double L = 0.25;
   double c[D + 1] = {0};
@@ -85,8 +86,9 @@ void fit_alpha(double g0sq, mimo::TrialParams& p) {
     }
   }
   double sc = 1.0;
-  for (int i = 0; i <= D; ++i, sc /= L) p.apoly[i] = (float)(mono[i] * sc);
-  p.alpha_xlim = (float)L;
+  using R = std::remove_reference_t<decltype(p.apoly[0])>;
+  for (int i = 0; i <= D; ++i, sc /= L) p.apoly[i] = (R)(mono[i] * sc);
+  p.alpha_xlim = (R)L;
 }
 
 }  // namespace
@@ -105,9 +107,12 @@ struct mimo_engine {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  float2* d_tw[2] = {nullptr, nullptr};  // stage twiddles for team_size(F), alt_team_size(F)
+  float2* d_tw[2] = {nullptr, nullptr};  // fp32 stage twiddles for team_size(F), alt_team_size(F)
+  double2* d_tw64 = nullptr;              // fp64 stage twiddles for team_size64(F)
   float* d_ant_rel = nullptr;
   float* d_f_rel = nullptr;
+  double* d_ant_rel64 = nullptr;
+  double* d_f_rel64 = nullptr;
   double* d_f_over_c = nullptr;
   double* d_tx_pos = nullptr;
   uint32_t* d_counts = nullptr;
@@ -125,12 +130,21 @@ int team_for(int F) { return mimo::team_size(F); }
 mimo::InstanceKey select_instance(const mimo_engine* e, bool csi) {
   mimo::InstanceKey k{};
   k.F = e->cfg.n_fft;
+  k.f64 = e->cfg.precision != MIMO_PREC_F32;
   const int S = e->cfg.n_sub_carr;
   auto aligned_at = [&](int T) {
     const int P = k.F / T;
     return (S % (4 * T) == 0) && S < k.F && (S / T == 8 || S / T == 4) && (S / T) < P;
   };
-  k.T = team_for(k.F);
+  k.T = k.f64 ? mimo::team_size64(k.F) : team_for(k.F);
+  if (k.f64) {  // one team size per fp64 instance
+    const int P = k.F / k.T;
+    k.aligned = aligned_at(k.T);
+    k.nslot = k.aligned ? S / k.T : P;
+    k.ch = e->cfg.channel_kind;
+    k.csi = csi;
+    return k;
+  }
   // Unaligned bands (S % 4T != 0) run the generic predicated path with P slots per
   // thread; the alternative team has half the points per thread, which measured 1.5x
   // faster there (60.7 vs 40.7 ms at S = 1000, F = 2048; profiles/r01/ab_generic.json).
@@ -147,24 +161,37 @@ mimo::InstanceKey select_instance(const mimo_engine* e, bool csi) {
   return k;
 }
 
-hipError_t launch(const mimo::InstanceKey& k, dim3 grid, hipStream_t st, const mimo::TrialParams& p, bool* found) {
+template <typename R>
+hipError_t launch(const mimo::InstanceKey& k, dim3 grid, hipStream_t st, const mimo::TrialParams<R>& p, bool* found) {
+  constexpr bool F64 = sizeof(R) == 8;
+#define MIMO_LAUNCH_F(FV)                                                                    \
+  if constexpr (F64) return mimo::launch_trial_F##FV##_f64(k, grid, st, p, found);           \
+  else return mimo::launch_trial_F##FV##_f32(k, grid, st, p, found);
 #ifdef MIMO_ONLY_F  // single-size diagnostic / A-B builds (Makefile targets ablation, variant)
-#define MIMO_ONLY_CAT2(a, b) a##b
-#define MIMO_ONLY_CAT(a, b) MIMO_ONLY_CAT2(a, b)
-  if (k.F == MIMO_ONLY_F) return mimo::MIMO_ONLY_CAT(launch_trial_F, MIMO_ONLY_F)(k, grid, st, p, found);
+  if (k.F == MIMO_ONLY_F) {
+#if MIMO_ONLY_F == 2048
+    MIMO_LAUNCH_F(2048)
+#elif MIMO_ONLY_F == 4096
+    MIMO_LAUNCH_F(4096)
+#elif MIMO_ONLY_F == 8192
+    MIMO_LAUNCH_F(8192)
+#endif
+  }
   *found = false;
   return hipSuccess;
-#endif
+#else
   switch (k.F) {
-    case 128: return mimo::launch_trial_F128(k, grid, st, p, found);
-    case 256: return mimo::launch_trial_F256(k, grid, st, p, found);
-    case 512: return mimo::launch_trial_F512(k, grid, st, p, found);
-    case 1024: return mimo::launch_trial_F1024(k, grid, st, p, found);
-    case 2048: return mimo::launch_trial_F2048(k, grid, st, p, found);
-    case 4096: return mimo::launch_trial_F4096(k, grid, st, p, found);
-    case 8192: return mimo::launch_trial_F8192(k, grid, st, p, found);
+    case 128: MIMO_LAUNCH_F(128)
+    case 256: MIMO_LAUNCH_F(256)
+    case 512: MIMO_LAUNCH_F(512)
+    case 1024: MIMO_LAUNCH_F(1024)
+    case 2048: MIMO_LAUNCH_F(2048)
+    case 4096: MIMO_LAUNCH_F(4096)
+    case 8192: MIMO_LAUNCH_F(8192)
     default: *found = false; return hipSuccess;
   }
+#endif
+#undef MIMO_LAUNCH_F
 }
 
 int validate_config(const mimo_config* c) {
@@ -182,6 +209,8 @@ int validate_config(const mimo_config* c) {
   if (c->receiver_kind != MIMO_RX_CNC && c->receiver_kind != MIMO_RX_MCNC)
     return fail(MIMO_EINVAL, "unknown receiver_kind");
   if (!c->tx_pos) return fail(MIMO_EINVAL, "tx_pos is required");
+  if (c->precision != MIMO_PREC_F64 && c->precision != MIMO_PREC_F32)
+    return fail(MIMO_EINVAL, "precision must be MIMO_PREC_F64 or MIMO_PREC_F32");
   return MIMO_OK;
 }
 
@@ -195,30 +224,35 @@ int ensure_device(mimo_engine* e) {
   const int F = e->cfg.n_fft, S = e->cfg.n_sub_carr, A = e->cfg.n_ant;
   // team-FFT stage twiddles per team size (team_fft.h plan), computed in double:
   // stage s, entry [r][jm] = exp(-j 2 pi e / F) with e = jm r F / (NS R)
-  std::vector<float2> tws[2];
-  const int teams[2] = {mimo::team_size(F), mimo::alt_team_size(F)};
-  for (int v = 0; v < 2; ++v) {
-    const int P = F / teams[v];
-    tws[v].assign(std::max(1, mimo::fft_tw_total(F, P)), make_float2(0.f, 0.f));
+  auto twiddles = [F](int T, auto cvt) {
+    const int P = F / T;
+    using V = decltype(cvt(0.0, 0.0));
+    std::vector<V> tw(std::max(1, mimo::fft_tw_total(F, P)), cvt(0.0, 0.0));
     for (int st = 1; st < mimo::fft_nst(F, P); ++st) {
       const int NS = 1 << mimo::fft_bits_before(F, P, st), R = 1 << mimo::fft_bits(F, P, st);
-      float2* blk = tws[v].data() + mimo::fft_tw_off(F, P, st);
+      V* blk = tw.data() + mimo::fft_tw_off(F, P, st);
       for (int r = 0; r < R; ++r)
         for (int jm = 0; jm < NS; ++jm) {
           const long e_idx = (long)jm * r * (F / (NS * R));
           const double ang = -2.0 * M_PI * (double)e_idx / (double)F;
-          blk[r * NS + jm] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+          blk[r * NS + jm] = cvt(std::cos(ang), std::sin(ang));
         }
     }
-  }
+    return tw;
+  };
+  auto to_f32 = [](double c, double s) { return make_float2((float)c, (float)s); };
+  auto to_f64 = [](double c, double s) { return make_double2(c, s); };
+  std::vector<float2> tws[2] = {twiddles(mimo::team_size(F), to_f32), twiddles(mimo::alt_team_size(F), to_f32)};
+  std::vector<double2> tw64 = twiddles(mimo::team_size64(F), to_f64);
   // in-band sub-carrier k -> bin (modulation.py:266-267)
   std::vector<float> f_rel(S);
-  std::vector<double> f_over_c(S);
+  std::vector<double> f_rel64(S), f_over_c(S);
   const double fc = e->freqs[0];  // bin 0 = centre frequency
   for (int k = 0; k < S; ++k) {
     const int bin = k < S / 2 ? F - S / 2 + k : k - S / 2 + 1;
     const double f = e->freqs[bin];
-    f_rel[k] = (float)(fc / f);
+    f_rel64[k] = fc / f;
+    f_rel[k] = (float)f_rel64[k];
     f_over_c[k] = f / kSpeedOfLight;
   }
   // Rayleigh FSPL at the nominal RX (channel.py:216-225), relative to the nearest antenna
@@ -232,12 +266,22 @@ int ensure_device(mimo_engine* e) {
   }
   e->d0 = dmin > 0 ? dmin : 1.0;
   std::vector<float> ant_rel(A);
-  for (int a = 0; a < A; ++a) ant_rel[a] = (float)(e->d0 / dist[a]);
+  std::vector<double> ant_rel64(A);
+  for (int a = 0; a < A; ++a) {
+    ant_rel64[a] = e->d0 / dist[a];
+    ant_rel[a] = (float)ant_rel64[a];
+  }
 
   for (int v = 0; v < 2; ++v) {
     HIP_TRY(hipMalloc(&e->d_tw[v], sizeof(float2) * tws[v].size()));
     HIP_TRY(hipMemcpy(e->d_tw[v], tws[v].data(), sizeof(float2) * tws[v].size(), hipMemcpyHostToDevice));
   }
+  HIP_TRY(hipMalloc(&e->d_tw64, sizeof(double2) * tw64.size()));
+  HIP_TRY(hipMemcpy(e->d_tw64, tw64.data(), sizeof(double2) * tw64.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&e->d_f_rel64, sizeof(double) * S));
+  HIP_TRY(hipMalloc(&e->d_ant_rel64, sizeof(double) * A));
+  HIP_TRY(hipMemcpy(e->d_f_rel64, f_rel64.data(), sizeof(double) * S, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_ant_rel64, ant_rel64.data(), sizeof(double) * A, hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&e->d_f_rel, sizeof(float) * S));
   HIP_TRY(hipMalloc(&e->d_f_over_c, sizeof(double) * S));
   HIP_TRY(hipMalloc(&e->d_ant_rel, sizeof(float) * A));
@@ -320,11 +364,40 @@ int32_t mimo_engine_run(mimo_engine* e, uint64_t seed, uint64_t first_trial, uin
   const mimo::InstanceKey key = select_instance(e, csi);
   if (int rc = ensure_device(e)) return rc;
 
-  mimo::TrialParams p{};
+  if (!c.reroll_chan && c.channel_kind != MIMO_CH_RAYLEIGH) {
+    // fixed RX: jitter span 0 around (x0, x0); only consistent when rx_y == rx_x
+    if (c.rx_pos[1] != c.rx_pos[0]) return fail(MIMO_EINVAL, "reroll_chan=0 requires rx_pos[1] == rx_pos[0]");
+  }
+  char buf[160];
+  snprintf(buf, sizeof buf, "F=%d T=%d slots=%d %s ch=%d csi=%d %s", key.F, key.T, key.nslot,
+           key.aligned ? "aligned" : "generic", key.ch, (int)key.csi, key.f64 ? "f64" : "f32");
+  e->desc = buf;
+
+  const uint64_t chunk_max = 1ull << 20;
+  const size_t need = (size_t)std::min<uint64_t>(n_trials, chunk_max) * n_idx;
+  if (need > e->counts_cap) {
+    if (e->d_counts) HIP_TRY(hipFree(e->d_counts));
+    HIP_TRY(hipMalloc(&e->d_counts, need * sizeof(uint32_t)));
+    e->counts_cap = need;
+  }
+  HIP_TRY(hipMemsetAsync(e->d_tot, 0, sizeof(unsigned long long) * n_idx, e->stream));
+  double ms_total = 0.0;
+
+  // Kernel parameters in the instance's arithmetic type, then the batch launches.
+  auto run_as = [&](auto zero) -> int {
+  using R = decltype(zero);
+  constexpr bool F64 = sizeof(R) == 8;
+  mimo::TrialParams<R> p{};
   p.seed = seed;
-  p.tw = e->d_tw[key.T == mimo::team_size(c.n_fft) ? 0 : 1];
-  p.ant_rel = e->d_ant_rel;
-  p.f_rel = e->d_f_rel;
+  if constexpr (F64) {
+    p.tw = e->d_tw64;
+    p.ant_rel = e->d_ant_rel64;
+    p.f_rel = e->d_f_rel64;
+  } else {
+    p.tw = e->d_tw[key.T == mimo::team_size(c.n_fft) ? 0 : 1];
+    p.ant_rel = e->d_ant_rel;
+    p.f_rel = e->d_f_rel;
+  }
   p.f_over_c = e->d_f_over_c;
   p.tx_pos = e->d_tx_pos;
   p.n_ant = c.n_ant;
@@ -335,23 +408,23 @@ int32_t mimo_engine_run(mimo_engine* e, uint64_t seed, uint64_t first_trial, uin
   p.label_mask = (uint32_t)c.constel_size - 1u;
   p.pa_kind = pt.pa_kind;
   p.cnc_pa_kind = pt.cnc_pa_kind;
-  p.sat_tx = (float)pt.sat_pow;
-  p.sqrt_sat_tx = (float)std::sqrt(std::max(pt.sat_pow, 0.0));
-  p.inv_sat_tx = pt.sat_pow > 0 ? (float)(1.0 / pt.sat_pow) : 0.f;
-  p.rapp_p = (float)pt.p_hardness;
-  p.toi_tx = (float)pt.toi_coeff;
-  p.sat_cnc = (float)pt.cnc_sat_pow;
-  p.sqrt_sat_cnc = (float)std::sqrt(std::max(pt.cnc_sat_pow, 0.0));
-  p.inv_sat_cnc = pt.cnc_sat_pow > 0 ? (float)(1.0 / pt.cnc_sat_pow) : 0.f;
-  p.toi_cnc = (float)pt.cnc_toi_coeff;
-  p.inv_alpha_cnc = (float)(1.0 / pt.cnc_alpha);
-  p.alpha_c = (float)(std::pow(10.0, pt.ibo_db / 10.0) * c.n_sub_carr / c.n_ant);
+  p.sat_tx = (R)pt.sat_pow;
+  p.sqrt_sat_tx = (R)std::sqrt(std::max(pt.sat_pow, 0.0));
+  p.inv_sat_tx = pt.sat_pow > 0 ? (R)(1.0 / pt.sat_pow) : R(0);
+  p.rapp_p = (R)pt.p_hardness;
+  p.toi_tx = (R)pt.toi_coeff;
+  p.sat_cnc = (R)pt.cnc_sat_pow;
+  p.sqrt_sat_cnc = (R)std::sqrt(std::max(pt.cnc_sat_pow, 0.0));
+  p.inv_sat_cnc = pt.cnc_sat_pow > 0 ? (R)(1.0 / pt.cnc_sat_pow) : R(0);
+  p.toi_cnc = (R)pt.cnc_toi_coeff;
+  p.inv_alpha_cnc = (R)(1.0 / pt.cnc_alpha);
+  p.alpha_c = (R)(std::pow(10.0, pt.ibo_db / 10.0) * c.n_sub_carr / c.n_ant);
   fit_alpha(std::pow(10.0, pt.ibo_db / 10.0), p);
-  p.inv_vk0 = (float)((double)c.n_ant / c.n_sub_carr);
-  p.es_over_snr = (float)(pt.avg_symbol_power / std::pow(10.0, pt.snr_db / 10.0));
-  p.csi_a = csi ? (float)std::sqrt(1.0 - pt.csi_eps * pt.csi_eps) : 1.f;
-  p.csi_b = csi ? (float)pt.csi_eps : 0.f;
-  p.inv_sqrt_f = (float)(1.0 / std::sqrt((double)c.n_fft));
+  p.inv_vk0 = (R)((double)c.n_ant / c.n_sub_carr);
+  p.es_over_snr = (R)(pt.avg_symbol_power / std::pow(10.0, pt.snr_db / 10.0));
+  p.csi_a = csi ? (R)std::sqrt(1.0 - pt.csi_eps * pt.csi_eps) : R(1);
+  p.csi_b = csi ? (R)pt.csi_eps : R(0);
+  p.inv_sqrt_f = (R)(1.0 / std::sqrt((double)c.n_fft));
   p.receiver = c.receiver_kind;
   p.max_iter = max_iter;
   p.rec_mask = rec_mask;
@@ -365,25 +438,6 @@ int32_t mimo_engine_run(mimo_engine* e, uint64_t seed, uint64_t first_trial, uin
 #ifdef MIMO_ABLATION
   if (const char* env = std::getenv("MIMO_ABLATE")) p.ablate = (uint32_t)std::strtoul(env, nullptr, 0);
 #endif
-  if (!c.reroll_chan && c.channel_kind != MIMO_CH_RAYLEIGH) {
-    // fixed RX: jitter span 0 around (x0, x0); only consistent when rx_y == rx_x
-    if (c.rx_pos[1] != c.rx_pos[0]) return fail(MIMO_EINVAL, "reroll_chan=0 requires rx_pos[1] == rx_pos[0]");
-  }
-
-  char buf[160];
-  snprintf(buf, sizeof buf, "F=%d T=%d slots=%d %s ch=%d csi=%d", key.F, key.T, key.nslot,
-           key.aligned ? "aligned" : "generic", key.ch, (int)key.csi);
-  e->desc = buf;
-
-  const uint64_t chunk_max = 1ull << 20;
-  const size_t need = (size_t)std::min<uint64_t>(n_trials, chunk_max) * n_idx;
-  if (need > e->counts_cap) {
-    if (e->d_counts) HIP_TRY(hipFree(e->d_counts));
-    HIP_TRY(hipMalloc(&e->d_counts, need * sizeof(uint32_t)));
-    e->counts_cap = need;
-  }
-  HIP_TRY(hipMemsetAsync(e->d_tot, 0, sizeof(unsigned long long) * n_idx, e->stream));
-  double ms_total = 0.0;
   for (uint64_t done = 0; done < n_trials; done += chunk_max) {
     const uint64_t nt = std::min<uint64_t>(chunk_max, n_trials - done);
     p.first_trial = first_trial + done;
@@ -404,6 +458,9 @@ int32_t mimo_engine_run(mimo_engine* e, uint64_t seed, uint64_t first_trial, uin
     HIP_TRY(hipEventElapsedTime(&ms, e->ev0, e->ev1));
     ms_total += ms;
   }
+  return MIMO_OK;
+  };
+  if (int rc = key.f64 ? run_as(0.0) : run_as(0.0f)) return rc;
   unsigned long long tot[64];
   HIP_TRY(hipMemcpyAsync(tot, e->d_tot, sizeof(unsigned long long) * n_idx, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -423,8 +480,8 @@ const char* mimo_engine_describe(const mimo_engine* e) {
   if (e->desc.empty()) {
     const mimo::InstanceKey k = select_instance(e, e->have_point && e->pt.csi_eps >= 0);
     char buf[160];
-    snprintf(buf, sizeof buf, "F=%d T=%d slots=%d %s ch=%d csi=%d", k.F, k.T, k.nslot,
-             k.aligned ? "aligned" : "generic", k.ch, (int)k.csi);
+    snprintf(buf, sizeof buf, "F=%d T=%d slots=%d %s ch=%d csi=%d %s", k.F, k.T, k.nslot,
+             k.aligned ? "aligned" : "generic", k.ch, (int)k.csi, k.f64 ? "f64" : "f32");
     const_cast<mimo_engine*>(e)->desc = buf;
   }
   return e->desc.c_str();
@@ -437,6 +494,9 @@ void mimo_engine_destroy(mimo_engine* e) {
     (void)hipFree(e->d_tw[0]);
     (void)hipFree(e->d_tw[1]);
     (void)hipFree(e->d_f_rel);
+    (void)hipFree(e->d_tw64);
+    (void)hipFree(e->d_f_rel64);
+    (void)hipFree(e->d_ant_rel64);
     (void)hipFree(e->d_f_over_c);
     (void)hipFree(e->d_ant_rel);
     (void)hipFree(e->d_tx_pos);

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "real.h"
+
 namespace mimo {
 
 enum Stream : uint32_t { ST_BITS = 1, ST_CHAN = 2, ST_NOISE = 3, ST_CSI = 4, ST_LOC = 5 };
@@ -51,10 +53,31 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, Key key) {
 }
 
 // Box-Muller on two words -> CN(0,1):  sqrt(-ln u1) * exp(j 2 pi u2),
-// u1 = (w0 + 0.5) 2^-32, u2 = w1 2^-32.  v_sin/v_cos take revolutions, so 2*pi*u2 is
-// never formed; v_log is log2.
-// c = -ln(2) scale^2 returns scale * CN(0,1) at no extra cost (v_log is log2).
+// u1 = (w0 + 0.5) 2^-32, u2 = w1 2^-32 (oracle/philox.py box_muller).
+//
+// fp32: v_sin/v_cos take revolutions, so 2*pi*u2 is never formed; v_log is log2, and the
+// scale argument c = -ln(2) scale^2 returns scale * CN(0,1) at no extra cost.
+// fp64: full-precision software ln / sincos (real.h); c = -scale^2 (natural log).
+// bm_c<R>(scale^2) builds c for either.
 constexpr float kNegLn2 = -0.69314718055994531f;
+template <typename R>
+__device__ __forceinline__ R bm_c(R scale2);
+template <>
+__device__ __forceinline__ float bm_c<float>(float scale2) {
+  return kNegLn2 * scale2;
+}
+template <>
+__device__ __forceinline__ double bm_c<double>(double scale2) {
+  return -scale2;
+}
+
+__device__ __forceinline__ float bm_log(uint32_t w0, float) {
+  return __builtin_amdgcn_logf(fmaf((float)w0, 2.3283064365386963e-10f, 1.1641532182693481e-10f));
+}
+__device__ __forceinline__ double bm_log(uint32_t w0, double) {
+  return ln_pos(((double)w0 + 0.5) * 2.3283064365386963e-10);  // exact argument
+}
+
 __device__ __forceinline__ float2 box_muller(uint32_t w0, uint32_t w1, float c = kNegLn2) {
   const float u1 = fmaf((float)w0, 2.3283064365386963e-10f, 1.1641532182693481e-10f);
   const float u2 = (float)w1 * 2.3283064365386963e-10f;
@@ -64,21 +87,29 @@ __device__ __forceinline__ float2 box_muller(uint32_t w0, uint32_t w1, float c =
   const float rho = __builtin_amdgcn_sqrtf(c * __builtin_amdgcn_logf(u1));
   return make_float2(rho * __builtin_amdgcn_cosf(u2), rho * __builtin_amdgcn_sinf(u2));
 }
+__device__ __forceinline__ double2 box_muller(uint32_t w0, uint32_t w1, double c) {
+  const double rho = __builtin_sqrt(c * bm_log(w0, 0.0));
+  double s, co;
+  sincos_rev((double)w1 * 2.3283064365386963e-10, s, co);  // exact revolutions
+  return make_double2(rho * co, rho * s);
+}
 
-__device__ __forceinline__ void cn_pair(Key key, uint32_t q, uint32_t trial, uint32_t stream, uint32_t aux,
-                                        float2& z1, float2& z2, float c = kNegLn2) {
+template <class C>
+__device__ __forceinline__ void cn_pair(Key key, uint32_t q, uint32_t trial, uint32_t stream, uint32_t aux, C& z1,
+                                        C& z2, real_of<C> c) {
   const uint4 w = philox4x32_10(make_uint4(q, trial, stream, aux), key);
   z1 = box_muller(w.x, w.y, c);
   z2 = box_muller(w.z, w.w, c);
 }
 
-// |z1|^2, |z2|^2 of cn_pair's draws without forming them: rho^2 = c log2(u1) (one v_log
+// |z1|^2, |z2|^2 of cn_pair's draws without forming them: rho^2 = c log(u1) (one log
 // per draw; no sqrt / sin / cos).  MRT norms only need the channel power.
-__device__ __forceinline__ void cn_pair_pow(Key key, uint32_t q, uint32_t trial, uint32_t stream, uint32_t aux,
-                                            float& p1, float& p2, float c = kNegLn2) {
+template <typename R>
+__device__ __forceinline__ void cn_pair_pow(Key key, uint32_t q, uint32_t trial, uint32_t stream, uint32_t aux, R& p1,
+                                            R& p2, R c) {
   const uint4 w = philox4x32_10(make_uint4(q, trial, stream, aux), key);
-  p1 = c * __builtin_amdgcn_logf(fmaf((float)w.x, 2.3283064365386963e-10f, 1.1641532182693481e-10f));
-  p2 = c * __builtin_amdgcn_logf(fmaf((float)w.z, 2.3283064365386963e-10f, 1.1641532182693481e-10f));
+  p1 = c * bm_log(w.x, R(0));
+  p2 = c * bm_log(w.z, R(0));
 }
 
 // Quarter pairing: sub-carrier k -> pair index q and slot (0: k1, 1: k2 = k1 + S/4).

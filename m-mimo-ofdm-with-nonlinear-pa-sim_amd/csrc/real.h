@@ -1,0 +1,155 @@
+// Precision traits of the fused trial kernel: one source, two arithmetic types.
+//
+// R = double is the reference's own precision (complex128 / float64 end to end,
+// modulation.py:270, noise.py:66); R = float is the fast variant.  Everything on the
+// signal chain (FFT, precoding, PA, channel, AGC, receiver) runs in R; the float
+// instances keep the hardware approximations (v_rsq / v_log / v_sin ...) that the
+// fp32 kernel was tuned with, the double instances use the full-precision software
+// forms below (gfx950 has no f64 transcendental instructions besides rcp / rsq / sqrt
+// seeds).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mimo {
+
+template <typename R>
+struct CxT;
+template <>
+struct CxT<float> {
+  using type = float2;
+};
+template <>
+struct CxT<double> {
+  using type = double2;
+};
+template <typename R>
+using cx = typename CxT<R>::type;
+template <class C>
+struct RealOf;
+template <>
+struct RealOf<float2> {
+  using type = float;
+};
+template <>
+struct RealOf<double2> {
+  using type = double;
+};
+template <class C>
+using real_of = typename RealOf<C>::type;
+
+__device__ __forceinline__ float2 mkc(float a, float b) { return make_float2(a, b); }
+__device__ __forceinline__ double2 mkc(double a, double b) { return make_double2(a, b); }
+template <typename R>
+__device__ __forceinline__ cx<R> czero() {
+  return mkc(R(0), R(0));
+}
+__device__ __forceinline__ float fmar(float a, float b, float c) { return fmaf(a, b, c); }
+__device__ __forceinline__ double fmar(double a, double b, double c) { return fma(a, b, c); }
+__device__ __forceinline__ float minr(float a, float b) { return fminf(a, b); }
+__device__ __forceinline__ double minr(double a, double b) { return fmin(a, b); }
+__device__ __forceinline__ float absr(float a) { return fabsf(a); }
+__device__ __forceinline__ float floor_r(float a) { return floorf(a); }
+__device__ __forceinline__ double floor_r(double a) { return floor(a); }
+__device__ __forceinline__ double absr(double a) { return fabs(a); }
+
+// ---------------------------------------------------------------- fp32: hardware forms
+__device__ __forceinline__ float rsq_r(float x) { return __builtin_amdgcn_rsqf(x); }   // rsq(0) = inf
+__device__ __forceinline__ float sqrt_r(float x) { return __builtin_amdgcn_sqrtf(x); }  // raw v_sqrt (1 ulp)
+__device__ __forceinline__ float log2_r(float x) { return __builtin_amdgcn_logf(x); }
+__device__ __forceinline__ float exp2_r(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float rcp_r(float x) { return 1.0f / x; }
+__device__ __forceinline__ float sqrt_ieee(float x) { return __builtin_sqrtf(x); }  // correctly rounded
+
+// ---------------------------------------------------------------- fp64: software forms
+// 1/sqrt(x) for finite x > 0: v_rsq_f64 seed + two Newton steps.  (Callers select away
+// the result for x = 0, where the fp32 form returns inf.)
+__device__ __forceinline__ double rsq_r(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) y = fma(y, fma(-h * y, y, 0.5), y);
+  return y;
+}
+__device__ __forceinline__ double sqrt_r(double x) { return __builtin_sqrt(x); }
+__device__ __forceinline__ double sqrt_ieee(double x) { return __builtin_sqrt(x); }
+__device__ __forceinline__ double log2_r(double x) { return log2(x); }
+__device__ __forceinline__ double exp2_r(double x) { return exp2(x); }
+__device__ __forceinline__ double rcp_r(double x) { return 1.0 / x; }
+
+// Natural log of a positive normal double: x = m 2^e with m in [sqrt(1/2), sqrt(2)),
+// ln m = 2 atanh(s), s = (m - 1) / (m + 1), |s| <= 0.1716: the series to s^19 is below
+// 2^-54 relative.  ~25 VALU ops; <= 2 ulp.
+__device__ __forceinline__ double ln_pos(double x) {
+  int e = __builtin_amdgcn_frexp_exp(x);
+  double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
+  const bool lo = m < 0.70710678118654752440;
+  m = lo ? m + m : m;
+  e = lo ? e - 1 : e;
+  const double f = m - 1.0;
+  const double den = 2.0 + f;
+  double r = __builtin_amdgcn_rcp(den);  // Newton: r (2 - den r), twice
+  r = fma(r, fma(-den, r, 1.0), r);
+  r = fma(r, fma(-den, r, 1.0), r);
+  const double s = f * r;
+  const double z = s * s;
+  double q = 2.0 / 19;
+  q = fma(q, z, 2.0 / 17);
+  q = fma(q, z, 2.0 / 15);
+  q = fma(q, z, 2.0 / 13);
+  q = fma(q, z, 2.0 / 11);
+  q = fma(q, z, 2.0 / 9);
+  q = fma(q, z, 2.0 / 7);
+  q = fma(q, z, 2.0 / 5);
+  q = fma(q, z, 2.0 / 3);
+  const double lnm = fma(s * z, q, s + s);
+  constexpr double kLn2Hi = 6.93147180369123816490e-01;  // ln 2 with 21 trailing zero bits
+  constexpr double kLn2Lo = 1.90821492927058770002e-10;
+  const double de = (double)e;
+  return fma(de, kLn2Hi, fma(de, kLn2Lo, lnm));
+}
+
+// sin / cos of 2 pi r (r in revolutions, |r| < 2^20): quadrant n = rint(4 r) is split
+// off exactly (Sterbenz), phi = 2 pi (r - n/4) in [-pi/4, pi/4], Taylor to phi^15 / phi^16
+// (truncation < 0.6 ulp).  The fp32 kernel's v_sin / v_cos also take revolutions.
+__device__ __forceinline__ void sincos_rev(double r, double& sn, double& cs) {
+  const double n = __builtin_rint(4.0 * r);
+  const double phi = (r - 0.25 * n) * 6.28318530717958647693;
+  const double z = phi * phi;
+  double ps = -1.0 / 1307674368000.0;         // -1/15!
+  ps = fma(ps, z, 1.0 / 6227020800.0);        // 1/13!
+  ps = fma(ps, z, -1.0 / 39916800.0);         // -1/11!
+  ps = fma(ps, z, 1.0 / 362880.0);            // 1/9!
+  ps = fma(ps, z, -1.0 / 5040.0);
+  ps = fma(ps, z, 1.0 / 120.0);
+  ps = fma(ps, z, -1.0 / 6.0);
+  const double s = fma(phi * z, ps, phi);
+  double pc = 1.0 / 20922789888000.0;         // 1/16!
+  pc = fma(pc, z, -1.0 / 87178291200.0);      // -1/14!
+  pc = fma(pc, z, 1.0 / 479001600.0);         // 1/12!
+  pc = fma(pc, z, -1.0 / 3628800.0);          // -1/10!
+  pc = fma(pc, z, 1.0 / 40320.0);
+  pc = fma(pc, z, -1.0 / 720.0);
+  pc = fma(pc, z, 1.0 / 24.0);
+  pc = fma(pc, z, -0.5);
+  const double c = fma(z, pc, 1.0);
+  const int q = ((int)n) & 3;
+  // (sin, cos) of phi + q pi/2
+  const double s1 = (q & 1) ? c : s, c1 = (q & 1) ? s : c;
+  sn = (q & 2) ? -s1 : s1;
+  cs = ((q + 1) & 2) ? -c1 : c1;
+}
+__device__ __forceinline__ double sin_rev(double r) {
+  double s, c;
+  sincos_rev(r, s, c);
+  return s;
+}
+__device__ __forceinline__ double cos_rev(double r) {
+  double s, c;
+  sincos_rev(r, s, c);
+  return c;
+}
+__device__ __forceinline__ float sin_rev(float r) { return __builtin_amdgcn_sinf(r); }
+__device__ __forceinline__ float cos_rev(float r) { return __builtin_amdgcn_cosf(r); }
+
+}  // namespace mimo

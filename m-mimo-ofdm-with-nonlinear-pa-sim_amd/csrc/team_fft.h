@@ -1,4 +1,4 @@
-// Workgroup ("team") FFT for the fused trial kernel — gfx950, fp32.
+// Workgroup ("team") FFT for the fused trial kernel — gfx950, fp32 or fp64 (Re).
 //
 // Replaces the reference's per-antenna torch CPU FFTs (modulation.py:270,
 // utilities.py:329, corrector.py:93,98): ortho IFFT/FFT of one F-point OFDM symbol.
@@ -19,6 +19,8 @@
 // (e^{-j2pi nk/F}), +1 inverse.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include "real.h"
 
 #ifndef MIMO_DIAG_NOPREBAR
 #define MIMO_DIAG_NOPREBAR 0  // timing diagnostics only (wrong results); production = 0
@@ -85,51 +87,64 @@ constexpr int fft_tw_off(int F, int P, int s) {
 }
 constexpr int fft_tw_total(int F, int P) { return fft_tw_off(F, P, fft_nst(F, P)); }
 
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+template <class C>
+__device__ __forceinline__ C cadd(C a, C b) {
+  return mkc(a.x + b.x, a.y + b.y);
 }
-__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {  // a * conj(b)
-  return make_float2(fmaf(a.x, b.x, a.y * b.y), fmaf(a.y, b.x, -a.x * b.y));
+template <class C>
+__device__ __forceinline__ C csub(C a, C b) {
+  return mkc(a.x - b.x, a.y - b.y);
 }
-__device__ __forceinline__ float2 cmac(float2 acc, float2 a, float2 b) {  // acc + a * b, 4 FMAs
-  return make_float2(fmaf(a.x, b.x, fmaf(-a.y, b.y, acc.x)), fmaf(a.x, b.y, fmaf(a.y, b.x, acc.y)));
+template <class C>
+__device__ __forceinline__ C cmul(C a, C b) {
+  return mkc(fmar(a.x, b.x, -a.y * b.y), fmar(a.x, b.y, a.y * b.x));
 }
-__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+template <class C>
+__device__ __forceinline__ C cmulc(C a, C b) {  // a * conj(b)
+  return mkc(fmar(a.x, b.x, a.y * b.y), fmar(a.y, b.x, -a.x * b.y));
+}
+template <class C>
+__device__ __forceinline__ C cmac(C acc, C a, C b) {  // acc + a * b, 4 FMAs
+  return mkc(fmar(a.x, b.x, fmar(-a.y, b.y, acc.x)), fmar(a.x, b.y, fmar(a.y, b.x, acc.y)));
+}
+template <class C>
+__device__ __forceinline__ C cscale(C a, real_of<C> s) {
+  return mkc(a.x * s, a.y * s);
+}
 
 // x * exp(DIR * j * 2 pi * M / R) with the trivial angles resolved at compile time.
-template <int M, int R, int DIR>
-__device__ __forceinline__ float2 ctw(float2 x) {
+template <int M, int R, int DIR, class C>
+__device__ __forceinline__ C ctw(C x) {
+  using Re = real_of<C>;
   constexpr int m = ((M % R) + R) % R;
   if constexpr (m == 0) {
     return x;
   } else if constexpr (4 * m == R) {  // DIR * j
-    return DIR > 0 ? make_float2(-x.y, x.x) : make_float2(x.y, -x.x);
+    return DIR > 0 ? mkc(-x.y, x.x) : mkc(x.y, -x.x);
   } else if constexpr (2 * m == R) {
-    return make_float2(-x.x, -x.y);
+    return mkc(-x.x, -x.y);
   } else if constexpr (4 * m == 3 * R) {  // -DIR * j
-    return DIR > 0 ? make_float2(x.y, -x.x) : make_float2(-x.y, x.x);
+    return DIR > 0 ? mkc(x.y, -x.x) : mkc(-x.y, x.x);
   } else {
-    constexpr float c = (float)ct_cos(2.0 * kPi * m / R);
-    constexpr float s = (float)(DIR * ct_sin(2.0 * kPi * m / R));
-    return make_float2(fmaf(x.x, c, -x.y * s), fmaf(x.x, s, x.y * c));
+    constexpr Re c = (Re)ct_cos(2.0 * kPi * m / R);
+    constexpr Re s = (Re)(DIR * ct_sin(2.0 * kPi * m / R));
+    return mkc(fmar(x.x, c, -x.y * s), fmar(x.x, s, x.y * c));
   }
 }
 
 // a + b / a - b where inputs known to be zero at compile time (ZA, ZB) are skipped:
 // pruning the IFFT's structurally-zero out-of-band inputs.
-template <bool ZA, bool ZB>
-__device__ __forceinline__ float2 zadd(float2 a, float2 b) {
-  if constexpr (ZA && ZB) return make_float2(0.f, 0.f);
+template <bool ZA, bool ZB, class C>
+__device__ __forceinline__ C zadd(C a, C b) {
+  if constexpr (ZA && ZB) return czero<real_of<C>>();
   else if constexpr (ZA) return b;
   else if constexpr (ZB) return a;
   else return cadd(a, b);
 }
-template <bool ZA, bool ZB>
-__device__ __forceinline__ float2 zsub(float2 a, float2 b) {
-  if constexpr (ZA && ZB) return make_float2(0.f, 0.f);
-  else if constexpr (ZA) return make_float2(-b.x, -b.y);
+template <bool ZA, bool ZB, class C>
+__device__ __forceinline__ C zsub(C a, C b) {
+  if constexpr (ZA && ZB) return czero<real_of<C>>();
+  else if constexpr (ZA) return mkc(-b.x, -b.y);
   else if constexpr (ZB) return a;
   else return csub(a, b);
 }
@@ -144,8 +159,8 @@ struct Dft {
     for (int n2 = 0; n2 < r2; ++n2) m |= ((ZM >> (n1 + r1 * n2)) & 1u) << n2;
     return m;
   }
-  template <int N1, int R1, int R2>
-  static __device__ __forceinline__ void first_level(float2 (&sub)[R1][R2], const float2* v) {
+  template <int N1, int R1, int R2, class C>
+  static __device__ __forceinline__ void first_level(C (&sub)[R1][R2], const C* v) {
     if constexpr (N1 < R1) {
 #pragma unroll
       for (int n2 = 0; n2 < R2; ++n2) sub[N1][n2] = v[N1 + R1 * n2];
@@ -154,18 +169,19 @@ struct Dft {
     }
   }
 
-  static __device__ __forceinline__ void run(float2* v) {
+  template <class C>
+  static __device__ __forceinline__ void run(C* v) {
     if constexpr (R == 1) {
       return;
     } else if constexpr (R == 2) {
-      const float2 a = v[0], b = v[1];
+      const C a = v[0], b = v[1];
       v[0] = zadd<z(0), z(1)>(a, b);
       v[1] = zsub<z(0), z(1)>(a, b);
     } else if constexpr (R == 4) {
       constexpr bool z02 = z(0) && z(2), z13 = z(1) && z(3);
-      const float2 t0 = zadd<z(0), z(2)>(v[0], v[2]), t1 = zsub<z(0), z(2)>(v[0], v[2]);
-      const float2 t2 = zadd<z(1), z(3)>(v[1], v[3]);
-      const float2 t3 = z13 ? make_float2(0.f, 0.f) : ctw<1, 4, DIR>(zsub<z(1), z(3)>(v[1], v[3]));
+      const C t0 = zadd<z(0), z(2)>(v[0], v[2]), t1 = zsub<z(0), z(2)>(v[0], v[2]);
+      const C t2 = zadd<z(1), z(3)>(v[1], v[3]);
+      const C t3 = z13 ? czero<real_of<C>>() : ctw<1, 4, DIR>(zsub<z(1), z(3)>(v[1], v[3]));
       v[0] = zadd<z02, z13>(t0, t2);
       v[2] = zsub<z02, z13>(t0, t2);
       v[1] = zadd<z02, z13>(t1, t3);
@@ -173,12 +189,12 @@ struct Dft {
     } else {
       constexpr int R1 = (R >= 16) ? 4 : 2;
       constexpr int R2 = R / R1;
-      float2 sub[R1][R2];
+      C sub[R1][R2];
       first_level<0, R1, R2>(sub, v);
       Twid<R1, R2, 1, 0>::apply(sub);
 #pragma unroll
       for (int k2 = 0; k2 < R2; ++k2) {
-        float2 col[R1];
+        C col[R1];
 #pragma unroll
         for (int n1 = 0; n1 < R1; ++n1) col[n1] = sub[n1][k2];
         Dft<R1, DIR>::run(col);
@@ -206,8 +222,9 @@ struct Dft {
 };
 
 // ---------------------------------------------------------------- team FFT
-template <int F, int T, int NBUF = 2>
+template <int F, int T, int NBUF = 2, typename Re = float>
 struct TeamFft {
+  using C = cx<Re>;
   static constexpr int P = F / T;
   static constexpr int LOG_F = ilog2(F);
   static constexpr int LOG_P = ilog2(P);
@@ -226,22 +243,22 @@ struct TeamFft {
   static __host__ __device__ constexpr int pad(int e) { return e + (e >> psh(S)); }
   // Global-address-space load (the laundered table pointer would otherwise be generic
   // and compile to flat loads, which also count against lgkmcnt with the LDS traffic).
-  static __device__ __forceinline__ float2 opaque_tw(int r) {
-    float2 w = make_float2(0.6f, 0.8f * (float)(r & 1));
+  static __device__ __forceinline__ C opaque_tw(int r) {
+    C w = mkc(Re(0.6), Re(0.8) * (Re)(r & 1));
     asm volatile("" : "+v"(w.x), "+v"(w.y));
     return w;
   }
-  static __device__ __forceinline__ float2 gload(const float2* p, int i) {
-    typedef float v2f __attribute__((ext_vector_type(2)));
+  static __device__ __forceinline__ C gload(const C* p, int i) {
+    typedef Re v2f __attribute__((ext_vector_type(2)));
     const v2f v = ((const __attribute__((address_space(1))) v2f*)p)[i];
-    return make_float2(v.x, v.y);
+    return mkc(v.x, v.y);
   }
 
   // Twiddles of stage S for butterflies i > 0: jm_i = jm_0 + OFF_i with OFF_i = (T i) mod NS
   // (T and NS are powers of two, t < T), so w_i[r] = w_0[r] exp(-j 2 pi OFF_i r / (NS R)):
   // a compile-time rotation instead of a load.
   template <int N, int OFF, int R, int r = 1>
-  static __device__ __forceinline__ void tw_shift(float2 (&w)[R], const float2 (&w0)[R]) {
+  static __device__ __forceinline__ void tw_shift(C (&w)[R], const C (&w0)[R]) {
     if constexpr (r < R) {
       w[r] = ctw<OFF * r, N, -1>(w0[r]);
       tw_shift<N, OFF, R, r + 1>(w, w0);
@@ -257,20 +274,20 @@ struct TeamFft {
   }
 
   template <int S, int DIR, int I, uint32_t ZM>
-  static __device__ __forceinline__ void butterfly(float2 (&d)[P], float2* buf, const float2 (&w0)[1 << bits(S)],
+  static __device__ __forceinline__ void butterfly(C (&d)[P], C* buf, const C (&w0)[1 << bits(S)],
                                                    int t, bool no_xchg) {
     constexpr int R = 1 << bits(S);
     constexpr int NS = 1 << bits_before(S);
     constexpr int B = P / R;
     constexpr bool LAST = (S == NST - 1);
-    float2 v[R];
+    C v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) v[r] = d[I + r * B];
     const int j = t + T * I;
     const int jm = j & (NS - 1);
     if constexpr (NS > 1) {
       constexpr int OFF = (T * I) & (NS - 1);
-      float2 w[R];
+      C w[R];
       if constexpr (OFF == 0) {
 #pragma unroll
         for (int r = 1; r < R; ++r) w[r] = w0[r];
@@ -294,14 +311,14 @@ struct TeamFft {
       if constexpr (NBUF == 1 && I == 0 && !MIMO_DIAG_NOPREBAR) __syncthreads();
       // pad(base + r NS) == pad(base) + pad(r NS) for power-of-two NS, R, T (the
       // padding never splits a write group): one address per i, immediate offsets.
-      float2* wb = buf + pad<S>((j / NS) * NS * R + jm);
+      C* wb = buf + pad<S>((j / NS) * NS * R + jm);
 #pragma unroll
       for (int r = 0; r < R; ++r) wb[pad<S>(r * NS)] = v[r];
     }
   }
 
   template <int S, int DIR, uint32_t ZM, int I = 0>
-  static __device__ __forceinline__ void butterflies(float2 (&d)[P], float2* buf, const float2 (&w0)[1 << bits(S)],
+  static __device__ __forceinline__ void butterflies(C (&d)[P], C* buf, const C (&w0)[1 << bits(S)],
                                                      int t, bool no_xchg) {
     if constexpr (I < P / (1 << bits(S))) {
       butterfly<S, DIR, I, ZM>(d, buf, w0, t, no_xchg);
@@ -326,12 +343,13 @@ struct TeamFft {
   // exchange instead of stalling each stage's first twiddle multiply.
   static constexpr int kMaxB = 5;
   // Measured -1.1 % (F 2048), -1.5 % (F 4096), +0.9 % (F 8192: more stages held live).
-  static constexpr bool PREFETCH = MIMO_TW_PREFETCH && F <= 4096;
+  // fp64: off (the prefetched twiddles would hold ~32 more VGPRs across a transform).
+  static constexpr bool PREFETCH = MIMO_TW_PREFETCH && F <= 4096 && sizeof(Re) == 4;
   struct Base {
-    float2 v[NST][kMaxB];
+    C v[NST][kMaxB];
   };
   template <int S>
-  static __device__ __forceinline__ void load_base(Base& b, const float2* __restrict__ tw, int t) {
+  static __device__ __forceinline__ void load_base(Base& b, const C* __restrict__ tw, int t) {
     if constexpr (S < NST) {
       constexpr int R = 1 << bits(S);
       constexpr int NS = 1 << bits_before(S);
@@ -348,15 +366,15 @@ struct TeamFft {
   }
 
   template <int S, int DIR, int PAR, uint32_t ZM, typename Fill>
-  static __device__ __forceinline__ void stage(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
+  static __device__ __forceinline__ void stage(C (&d)[P], C* lds, const C* __restrict__ tw, int t,
                                                bool no_xchg, const Base& base, const Fill& fill) {
     constexpr int R = 1 << bits(S);
     constexpr int NS = 1 << bits_before(S);
     constexpr int B = P / R;
     constexpr bool LAST = (S == NST - 1);
     static_assert(B >= 1 && B * R == P, "radix must divide points per thread");
-    float2* buf = lds + (NBUF == 2 ? ((S + PAR) & 1) * LDS_ELEMS : 0);
-    float2 w0[R];
+    C* buf = lds + (NBUF == 2 ? ((S + PAR) & 1) * LDS_ELEMS : 0);
+    C w0[R];
     if constexpr (NS > 1 && PREFETCH) {
 #pragma unroll
       for (int r = 1; r < R; ++r) {
@@ -370,13 +388,13 @@ struct TeamFft {
       }
     } else if constexpr (NS > 1) {
       constexpr int TW_OFF = fft_tw_off(F, P, S);  // forced compile-time (a runtime call otherwise)
-      const float2* tws = tw + TW_OFF;
+      const C* tws = tw + TW_OFF;
       const int jm0 = t & (NS - 1);
 #pragma unroll
       for (int r = 1; r < R; ++r) {
         if (r == 1 || ((r & (r - 1)) == 0 && r > MIMO_TW_LOAD_MAX)) {
           w0[r] = r > 1 ? cmul(w0[r / 2], w0[r / 2])  // w(2r) = w(r)^2
-                  : MIMO_DIAG_NOTW == 1 ? make_float2(1.f, 0.f)  // diagnostic: no twiddle traffic
+                  : MIMO_DIAG_NOTW == 1 ? mkc(Re(1), Re(0))  // diagnostic: no twiddle traffic
                   : MIMO_DIAG_NOTW == 2 ? opaque_tw(r)            // diagnostic: multiplies, no loads
                                         : gload(tws + r * NS, jm0);
         } else if ((r & (r - 1)) == 0) {
@@ -392,7 +410,7 @@ struct TeamFft {
     if constexpr (!LAST) {
       if (!no_xchg) {
         __syncthreads();
-        const float2* rb = buf + pad<S>(t);
+        const C* rb = buf + pad<S>(t);
 #pragma unroll
         for (int m = 0; m < P; ++m) d[m] = rb[pad<S>(T * m)];
       }
@@ -403,7 +421,7 @@ struct TeamFft {
   }
 
   template <int S, int DIR, int PAR, uint32_t ZM, typename Fill>
-  static __device__ __forceinline__ void stages(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
+  static __device__ __forceinline__ void stages(C (&d)[P], C* lds, const C* __restrict__ tw, int t,
                                                 bool no_xchg, const Base& base, const Fill& fill) {
     if constexpr (S < NST) {
       stage<S, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base, fill);
@@ -429,9 +447,9 @@ struct TeamFft {
     __device__ __forceinline__ void operator()(int) const {}
   };
   template <int DIR, int PAR = 0, uint32_t ZM = 0, typename Fill = NoFill>
-  static __device__ __forceinline__ void run(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
+  static __device__ __forceinline__ void run(C (&d)[P], C* lds, const C* __restrict__ tw, int t,
                                              bool no_xchg = false, const Fill& fill = Fill{}) {
-    const float2* twl = tw;
+    const C* twl = tw;
     int tl = t;
     asm volatile("" : "+s"(twl));
     asm volatile("" : "+v"(tl));
@@ -441,7 +459,7 @@ struct TeamFft {
   }
   // IFFT then FFT of one antenna / CNC iteration: an even number of exchanges in total.
   template <int DIR, typename Fill = NoFill>
-  static __device__ __forceinline__ void run_second(float2 (&d)[P], float2* lds, const float2* __restrict__ tw, int t,
+  static __device__ __forceinline__ void run_second(C (&d)[P], C* lds, const C* __restrict__ tw, int t,
                                                     bool no_xchg = false, const Fill& fill = Fill{}) {
     run<DIR, XCHG & 1, 0u, Fill>(d, lds, tw, t, no_xchg, fill);
   }

@@ -1,8 +1,14 @@
-// Instantiates the fused trial kernel for one FFT size (compiled once per -DINST_F=...).
+// Instantiates the fused trial kernel for one FFT size and arithmetic type
+// (compiled once per -DINST_F=<size> -DINST_F64=<0|1>).
+#include <type_traits>
+
 #include "trial_launch.h"
 
 #ifndef INST_F
 #error "compile with -DINST_F=<fft size>"
+#endif
+#ifndef INST_F64
+#define INST_F64 0
 #endif
 
 #define MIMO_CAT2(a, b) a##b
@@ -12,8 +18,19 @@ namespace mimo {
 namespace {
 
 constexpr int kF = INST_F;
+constexpr bool kF64 = INST_F64 != 0;
+using Real = std::conditional_t<kF64, double, float>;
 #ifndef MIMO_TWOPATH_W2
 #define MIMO_TWOPATH_W2 0  // 1: two-path at 2 waves/SIMD (measured 12 % slower than 3)
+#endif
+#ifndef MIMO_F64_MINW
+#define MIMO_F64_MINW 2  // fp64 instances: waves/SIMD target, exchange buffers, symbols in LDS
+#endif
+#ifndef MIMO_F64_NBUF
+#define MIMO_F64_NBUF 1
+#endif
+#ifndef MIMO_F64_SYMW
+#define MIMO_F64_SYMW 1
 #endif
 #ifndef MIMO_MINW16
 #define MIMO_MINW16 3  // waves/SIMD target of the 16-point aligned instances (A/B knob)
@@ -33,6 +50,8 @@ struct Profile {
 };
 constexpr Profile profile_for(int T, bool aligned, int ch) {
   const int P = kF / T;
+  if (kF64 && kF >= 8192) return Profile{2, 1, false};  // 136 KiB exchange buffer: one team per CU
+  if (kF64) return Profile{MIMO_F64_MINW, MIMO_F64_NBUF, MIMO_F64_SYMW != 0};
   if (!aligned) return Profile{2, kF >= 4096 ? 1 : 2, true};  // one buffer from F = 4096: 2 teams/CU
   if (ch == CH_TWOPATH && MIMO_TWOPATH_W2) return Profile{2, 2, false};  // fp64 geometry: register-heavy
   if (P < 16) return Profile{4, 2, false};
@@ -41,14 +60,15 @@ constexpr Profile profile_for(int T, bool aligned, int ch) {
 }
 
 template <int T, int NSLOT, bool AL, int CH, bool CSI>
-hipError_t go(dim3 grid, hipStream_t st, const TrialParams& p) {
+hipError_t go(dim3 grid, hipStream_t st, const TrialParams<Real>& p) {
   constexpr Profile pr = profile_for(T, AL, CH);
-  hipLaunchKernelGGL((trial_kernel<kF, T, NSLOT, AL, CH, CSI, pr.minw, pr.nbuf, pr.symw_lds>), grid, dim3(T), 0, st, p);
+  hipLaunchKernelGGL((trial_kernel<Real, kF, T, NSLOT, AL, CH, CSI, pr.minw, pr.nbuf, pr.symw_lds>), grid, dim3(T), 0,
+                     st, p);
   return hipGetLastError();
 }
 
 template <int T, int NSLOT, bool AL>
-hipError_t by_channel(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams& p, bool* found) {
+hipError_t by_channel(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams<Real>& p, bool* found) {
   *found = true;
   switch (k.ch) {
     case CH_RAYLEIGH:
@@ -66,7 +86,7 @@ hipError_t by_channel(const InstanceKey& k, dim3 grid, hipStream_t st, const Tri
 }
 
 template <int T>
-hipError_t by_team(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams& p, bool* found) {
+hipError_t by_team(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams<Real>& p, bool* found) {
   constexpr int P = kF / T;
   if (k.aligned) {
     if constexpr (8 < P) {
@@ -83,13 +103,21 @@ hipError_t by_team(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialP
 
 }  // namespace
 
-hipError_t MIMO_CAT(launch_trial_F, INST_F)(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams& p,
-                                            bool* found) {
+#if INST_F64
+#define MIMO_LAUNCH_NAME MIMO_CAT(MIMO_CAT(launch_trial_F, INST_F), _f64)
+#else
+#define MIMO_LAUNCH_NAME MIMO_CAT(MIMO_CAT(launch_trial_F, INST_F), _f32)
+#endif
+hipError_t MIMO_LAUNCH_NAME(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams<Real>& p, bool* found) {
   *found = false;
-  if (k.F != kF) return hipSuccess;
-  if (k.T == team_size(kF)) return by_team<team_size(kF)>(k, grid, st, p, found);
-  if constexpr (alt_team_size(kF) != team_size(kF)) {
-    if (k.T == alt_team_size(kF)) return by_team<alt_team_size(kF)>(k, grid, st, p, found);
+  if (k.F != kF || k.f64 != kF64) return hipSuccess;
+  if constexpr (kF64) {
+    if (k.T == team_size64(kF)) return by_team<team_size64(kF)>(k, grid, st, p, found);
+  } else {
+    if (k.T == team_size(kF)) return by_team<team_size(kF)>(k, grid, st, p, found);
+    if constexpr (alt_team_size(kF) != team_size(kF)) {
+      if (k.T == alt_team_size(kF)) return by_team<alt_team_size(kF)>(k, grid, st, p, found);
+    }
   }
   return hipSuccess;
 }

@@ -55,28 +55,31 @@ constexpr int kMaxCsiAnt = 512;  // CSI-error runs: antennas (LDS per team; engi
 #define MIMO_VK_DPP 1  // per-antenna precoding-power wave sum by DPP (0: __shfl_xor)
 #endif
 
+template <typename R>
 struct TrialParams {
+  using C = cx<R>;
   uint64_t seed;
   uint64_t first_trial;
   uint32_t* counts;              // [n_trials][n_idx]
-  const float2* tw;              // team-FFT stage twiddles of (F, T) (team_fft.h fft_tw_off)
-  const float* ant_rel;          // [A]  d0 / d_a      (Rayleigh FSPL, relative)
-  const float* f_rel;            // [S]  fc / f_k      (f_k float32-quantised as in the reference)
+  const C* tw;                   // team-FFT stage twiddles of (F, T) (team_fft.h fft_tw_off)
+  const R* ant_rel;              // [A]  d0 / d_a      (Rayleigh FSPL, relative)
+  const R* f_rel;                // [S]  fc / f_k      (f_k float32-quantised as in the reference)
   const double* f_over_c;        // [S]  f_k / c       (LoS / two-path phases)
   const double* tx_pos;          // [A*3]
   int n_ant, n_sc, qam_l, half_bits;
   uint32_t label_mask;
   int pa_kind, cnc_pa_kind;
-  float sat_tx, sqrt_sat_tx, inv_sat_tx, rapp_p, toi_tx;
-  float sat_cnc, sqrt_sat_cnc, inv_sat_cnc, toi_cnc, inv_alpha_cnc;
-  float alpha_c;                 // 10^(IBO/10) S / A : gamma_a^2 = alpha_c / vk_pow[a]
+  R sat_tx, sqrt_sat_tx, inv_sat_tx, rapp_p, toi_tx;
+  R sat_cnc, sqrt_sat_cnc, inv_sat_cnc, toi_cnc, inv_alpha_cnc;
+  R alpha_c;                     // 10^(IBO/10) S / A : gamma_a^2 = alpha_c / vk_pow[a]
   // alpha(gamma_a^2) as a degree-8 polynomial in x = vk_pow[a] A / S - 1 on |x| <= alpha_xlim
-  // (host Chebyshev fit, ~1e-7 relative); the exact formula outside (engine.hip fit_alpha)
-  float apoly[9];
-  float inv_vk0, alpha_xlim;
-  float es_over_snr;             // Es / 10^(SNR/10)
-  float csi_a, csi_b;            // sqrt(1 - eps^2), eps
-  float inv_sqrt_f;
+  // (host Chebyshev fit, ~1e-7 relative); the exact formula outside (engine.hip fit_alpha).
+  // fp32 instances only: the fp64 instances always evaluate the exact formula.
+  R apoly[9];
+  R inv_vk0, alpha_xlim;
+  R es_over_snr;                 // Es / 10^(SNR/10)
+  R csi_a, csi_b;                // sqrt(1 - eps^2), eps
+  R inv_sqrt_f;
   int receiver;
   int max_iter;                  // largest iteration index to run (CNC / MCNC)
   uint32_t rec_mask;             // bit i: record iteration i
@@ -129,15 +132,17 @@ struct Slots {
     }
   }
 
-  static __device__ __forceinline__ void scatter(float2 (&d)[P], const float2 (&x)[NSLOT], bool t0) {
+  template <class C>
+  static __device__ __forceinline__ void scatter(C (&d)[P], const C (&x)[NSLOT], bool t0) {
+    using R = real_of<C>;
 #pragma unroll
-    for (int m = 0; m < P; ++m) d[m] = make_float2(0.f, 0.f);
+    for (int m = 0; m < P; ++m) d[m] = czero<R>();
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
       if constexpr (ALIGNED) {
         if (s == 0) {
-          d[0] = t0 ? make_float2(0.f, 0.f) : x[0];
-          d[HALF] = t0 ? x[0] : make_float2(0.f, 0.f);
+          d[0] = t0 ? czero<R>() : x[0];
+          d[HALF] = t0 ? x[0] : czero<R>();
           continue;
         }
       }
@@ -145,7 +150,8 @@ struct Slots {
     }
   }
 
-  static __device__ __forceinline__ float2 gather(const float2 (&d)[P], int s, bool t0) {
+  template <class C>
+  static __device__ __forceinline__ C gather(const C (&d)[P], int s, bool t0) {
     if constexpr (ALIGNED) {
       if (s == 0) return t0 ? d[HALF] : d[0];
     }
@@ -162,7 +168,8 @@ __device__ __forceinline__ V opaque(V v) {
   asm volatile("" : "+v"(v));
   return v;
 }
-__device__ __forceinline__ float wave_sum(float v) {
+template <typename R>
+__device__ __forceinline__ R wave_sum(R v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
@@ -171,13 +178,21 @@ __device__ __forceinline__ float wave_sum(float v) {
 // Wave sum delivered in lane 63 only (other lanes hold partial sums): DPP adds on the
 // VALU instead of the six dependent ds_bpermute round trips of __shfl_xor.  Per row of
 // 16 lanes: pair / quad swaps and the half-row / row mirrors give every lane its row sum;
-// row_bcast:15 then row_bcast:31 fold rows 0-2 into row 3.
+// row_bcast:15 then row_bcast:31 fold rows 0-2 into row 3.  (fp64: both halves moved.)
 template <int CTRL, int ROW_MASK = 0xF>
 __device__ __forceinline__ float dpp_add(float v) {
   const int s = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, false);
   return v + __builtin_bit_cast(float, s);
 }
-__device__ __forceinline__ float wave_sum_lane63(float v) {
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp_add(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, ROW_MASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, ROW_MASK, 0xF, false);
+  return v + __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <typename R>
+__device__ __forceinline__ R wave_sum_lane63(R v) {
   v = dpp_add<0xB1>(v);        // quad_perm [1,0,3,2]
   v = dpp_add<0x4E>(v);        // quad_perm [2,3,0,1]
   v = dpp_add<0x141>(v);       // row_half_mirror
@@ -188,8 +203,8 @@ __device__ __forceinline__ float wave_sum_lane63(float v) {
 }
 
 // Team-wide sum; every thread gets the result.  Two barriers.
-template <int T>
-__device__ __forceinline__ float team_sum(float v, float* red) {
+template <int T, typename R>
+__device__ __forceinline__ R team_sum(R v, R* red) {
   if constexpr (T == 64) {
     return wave_sum(v);
   } else {
@@ -197,7 +212,7 @@ __device__ __forceinline__ float team_sum(float v, float* red) {
     __syncthreads();
     if ((threadIdx.x & 63) == 63) red[threadIdx.x >> 6] = v;
     __syncthreads();
-    float s = 0.f;
+    R s = R(0);
 #pragma unroll
     for (int i = 0; i < T / 64; ++i) s += red[i];
     return s;
@@ -209,51 +224,57 @@ __device__ __forceinline__ float alpha_of_gamma2(float g2) {
   const float g = __builtin_sqrtf(g2);
   return 1.0f - __expf(-g2) + 0.88622692545275801f * g * erfcf(g);
 }
+__device__ __forceinline__ double alpha_of_gamma2(double g2) {
+  const double g = __builtin_sqrt(g2);
+  return 1.0 - exp(-g2) + 0.88622692545275801 * g * erfc(g);
+}
 
 // PA on one time-domain sample (distortion.py:9-19, 102-113, 202-211).
-__device__ __forceinline__ float2 pa_apply(int kind, float2 x, float sat, float sqrt_sat, float inv_sat, float rapp_p,
-                                           float toi) {
-  const float pw = fmaf(x.x, x.x, x.y * x.y);
-  float sc = 1.0f;
+// Soft limiter, fp32: min(1, sqrt(sat) rsq(pw)) (rsq(0) = inf -> 1); fp64: the
+// reference's branch |x|^2 > sat, then x sqrt(sat / |x|^2).
+template <class C, typename R = real_of<C>>
+__device__ __forceinline__ C pa_apply(int kind, C x, R sat, R sqrt_sat, R inv_sat, R rapp_p, R toi) {
+  const R pw = fmar(x.x, x.x, x.y * x.y);
+  R sc = R(1);
   if (kind == PA_SOFTLIM) {
-    sc = fminf(1.0f, sqrt_sat * __builtin_amdgcn_rsqf(pw));  // rsq(0) = inf -> 1
+    if constexpr (sizeof(R) == 4) sc = minr(1.0f, sqrt_sat * rsq_r(pw));
+    else sc = pw > sat ? sqrt_sat * rsq_r(pw) : R(1);
   } else if (kind == PA_RAPP) {
     // 1 / (1 + (pw/sat)^p)^(1/(2p))
-    const float u = pw * inv_sat;
-    const float up = u > 0.f ? __builtin_amdgcn_exp2f(rapp_p * __builtin_amdgcn_logf(u)) : 0.f;
-    sc = __builtin_amdgcn_exp2f(-(0.5f / rapp_p) * __builtin_amdgcn_logf(1.0f + up));
+    const R u = pw * inv_sat;
+    const R up = u > R(0) ? exp2_r(rapp_p * log2_r(u)) : R(0);
+    sc = exp2_r(-(R(0.5) / rapp_p) * log2_r(R(1) + up));
   } else if (kind == PA_TOI) {
-    sc = 1.0f - toi * pw;
+    sc = R(1) - toi * pw;
   }
-  return make_float2(x.x * sc, x.y * sc);
+  return mkc(x.x * sc, x.y * sc);
 }
 
 // Rapp with an integer hardness: (pw/sat)^p by multiplication (config 5 uses p = 3),
-// one v_log + one v_exp per sample instead of two of each.
-template <int IP, int P>
-__device__ __forceinline__ void rapp_int(float2 (&d)[P], float inv_sat) {
+// one log + one exp per sample instead of two of each.
+template <int IP, int P, class C, typename R = real_of<C>>
+__device__ __forceinline__ void rapp_int(C (&d)[P], R inv_sat) {
 #pragma unroll
   for (int m = 0; m < P; ++m) {
-    const float u = fmaf(d[m].x, d[m].x, d[m].y * d[m].y) * inv_sat;
-    float up = u;
+    const R u = fmar(d[m].x, d[m].x, d[m].y * d[m].y) * inv_sat;
+    R up = u;
 #pragma unroll
     for (int i = 1; i < IP; ++i) up *= u;
-    const float sc = __builtin_amdgcn_exp2f((-0.5f / IP) * __builtin_amdgcn_logf(1.0f + up));
-    d[m] = make_float2(d[m].x * sc, d[m].y * sc);
+    const R sc = exp2_r((R(-0.5) / IP) * log2_r(R(1) + up));
+    d[m] = mkc(d[m].x * sc, d[m].y * sc);
   }
 }
 
 // PA on all P samples of a thread: one uniform branch on the kind, then a straight loop.
-template <int P>
-__device__ __forceinline__ void pa_block(int kind, float2 (&d)[P], float sat, float sqrt_sat, float inv_sat,
-                                         float rapp_p, float toi) {
+template <int P, class C, typename R = real_of<C>>
+__device__ __forceinline__ void pa_block(int kind, C (&d)[P], R sat, R sqrt_sat, R inv_sat, R rapp_p, R toi) {
   if (kind == PA_SOFTLIM) {
 #pragma unroll
     for (int m = 0; m < P; ++m) d[m] = pa_apply(PA_SOFTLIM, d[m], sat, sqrt_sat, inv_sat, rapp_p, toi);
 #if MIMO_RAPP_INT
-  } else if (kind == PA_RAPP && rapp_p == 3.0f) {
+  } else if (kind == PA_RAPP && rapp_p == R(3)) {
     rapp_int<3>(d, inv_sat);
-  } else if (kind == PA_RAPP && rapp_p == 2.0f) {
+  } else if (kind == PA_RAPP && rapp_p == R(2)) {
     rapp_int<2>(d, inv_sat);
 #endif
   } else if (kind == PA_RAPP) {
@@ -275,9 +296,10 @@ __device__ __forceinline__ uint32_t gray_inv(uint32_t g) {
   g ^= g >> 8;
   return g;
 }
-__device__ __forceinline__ uint32_t slice_axis(float x, int L) {
-  const float q = (x + (float)L) * 0.5f;
-  float fi = floorf(q);
+template <typename R>
+__device__ __forceinline__ uint32_t slice_axis(R x, int L) {
+  const R q = (x + (R)L) * R(0.5);
+  const R fi = floor_r(q);
   int i = (int)fi;
   if (q == fi && i > 0 && i < L) {  // exact midpoint between levels i-1 and i
     i = gray((uint32_t)(i - 1)) < gray((uint32_t)i) ? i - 1 : i;
@@ -285,23 +307,27 @@ __device__ __forceinline__ uint32_t slice_axis(float x, int L) {
   i = i < 0 ? 0 : (i > L - 1 ? L - 1 : i);
   return gray((uint32_t)i);
 }
-__device__ __forceinline__ uint32_t slice(float2 z, int L, int hb) {
+template <class C>
+__device__ __forceinline__ uint32_t slice(C z, int L, int hb) {
   return (slice_axis(z.x, L) << hb) | slice_axis(z.y, L);
 }
-__device__ __forceinline__ float2 qam_point(uint32_t label, int L, int hb) {
+template <typename R>
+__device__ __forceinline__ cx<R> qam_point(uint32_t label, int L, int hb) {
   const uint32_t ii = gray_inv(label >> hb), iq = gray_inv(label & ((1u << hb) - 1u));
-  return make_float2((float)(2 * (int)ii - (L - 1)), (float)(2 * (int)iq - (L - 1)));
+  return mkc((R)(2 * (int)ii - (L - 1)), (R)(2 * (int)iq - (L - 1)));
 }
 
 // ---------------------------------------------------------------- channel generation
-template <int F, int T, int NSLOT, bool ALIGNED, int CH>
+template <typename R, int F, int T, int NSLOT, bool ALIGNED, int CH>
 struct Channel {
   using SL = Slots<F, T, NSLOT, ALIGNED>;
+  using C = cx<R>;
+  using Params = TrialParams<R>;
 
   // CN(0,1) draws of one stream for the thread's slots (pairs resolved in-thread when aligned).
-  // c = -ln(2) scale^2 scales the draws (box_muller).
+  // c = bm_c(scale^2) scales the draws (box_muller).
   static __device__ __forceinline__ void normals(Key key, uint32_t trial, uint32_t stream, uint32_t aux, int t, int S,
-                                                 float2 (&z)[NSLOT], float c = kNegLn2) {
+                                                 C (&z)[NSLOT], R c = bm_c<R>(R(1))) {
     if constexpr (ALIGNED) {
       // Pair indices in closed form (pair_of() applied to the aligned slot map):
       //   positive band, slots j and j + Q: q = S/4 - 1 + t + T j, except thread 0 /
@@ -312,7 +338,7 @@ struct Channel {
       const int qp = (S >> 2) - 1 + t;
 #pragma unroll
       for (int j = 0; j < Q; ++j) {
-        float2 z1, z2;
+        C z1, z2;
         const bool sw = (j == 0) && t0;
         cn_pair(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, stream, aux, z1, z2, c);
         z[j] = sw ? z2 : z1;
@@ -326,12 +352,12 @@ struct Channel {
       for (int s = 0; s < NSLOT; ++s) {
         bool v;
         const int k = SL::k_of(s, t, S, v);
-        z[s] = make_float2(0.f, 0.f);
+        z[s] = czero<R>();
         if (v) {
           uint32_t q;
           int slot;
           pair_of(k, S, q, slot);
-          float2 z1, z2;
+          C z1, z2;
           cn_pair(key, q, trial, stream, aux, z1, z2, c);
           z[s] = slot == 0 ? z1 : z2;
         }
@@ -344,11 +370,11 @@ struct Channel {
   // negative band (band 1).  normals() == all 2 Q chunks.
   static constexpr int kChunks = ALIGNED ? SL::HALF : 0;
   static __device__ __forceinline__ void normals_chunk(int c, Key key, uint32_t trial, uint32_t stream, uint32_t aux,
-                                                       int t, int S, float2 (&z)[NSLOT], float cs) {
+                                                       int t, int S, C (&z)[NSLOT], R cs) {
     if constexpr (ALIGNED) {
       constexpr int Q = SL::HALF / 2;
       const int j = c >> 1;
-      float2 z1, z2;
+      C z1, z2;
       if ((c & 1) == 0) {
         const bool sw = (j == 0) && (t == 0);
         cn_pair(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)((S >> 2) - 1 + t + T * j), trial, stream, aux, z1, z2,
@@ -365,18 +391,18 @@ struct Channel {
 
   // |H|^2 of antenna a at the thread's slots (Rayleigh, FSPL factor f_rel left out as in
   // gen<false>): the same draws as gen(), magnitudes only.
-  static __device__ __forceinline__ void power(const TrialParams& p, Key key, uint32_t trial, int a, int t,
-                                               float (&e2)[NSLOT]) {
+  static __device__ __forceinline__ void power(const Params& p, Key key, uint32_t trial, int a, int t,
+                                               R (&e2)[NSLOT]) {
     const int S = p.n_sc;
-    const float sa = p.ant_rel[a];
-    const float c = kNegLn2 * (sa * sa);
+    const R sa = p.ant_rel[a];
+    const R c = bm_c<R>(sa * sa);
     if constexpr (ALIGNED) {
       constexpr int Q = SL::HALF / 2;
       const bool t0 = (t == 0);
       const int qp = (S >> 2) - 1 + t;
 #pragma unroll
       for (int j = 0; j < Q; ++j) {
-        float p1, p2;
+        R p1, p2;
         const bool sw = (j == 0) && t0;
         cn_pair_pow(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, ST_CHAN, (uint32_t)a, p1, p2,
                     c);
@@ -391,12 +417,12 @@ struct Channel {
       for (int s = 0; s < NSLOT; ++s) {
         bool v;
         const int k = SL::k_of(s, t, S, v);
-        e2[s] = 0.f;
+        e2[s] = R(0);
         if (v) {
           uint32_t q;
           int slot;
           pair_of(k, S, q, slot);
-          float p1, p2;
+          R p1, p2;
           cn_pair_pow(key, q, trial, ST_CHAN, (uint32_t)a, p1, p2, c);
           e2[s] = slot == 0 ? p1 : p2;
         }
@@ -409,59 +435,59 @@ struct Channel {
   // per-sub-carrier FSPL factor fc/f_k, which the kernel then applies once per trial
   // (it cancels in the MRT precoder; see the kernel's AWGN step).
   template <bool FREL>
-  static __device__ __forceinline__ void gen(const TrialParams& p, Key key, uint32_t trial, int a, int t,
-                                             const double (&rx)[3], float2 (&h)[NSLOT]) {
+  static __device__ __forceinline__ void gen(const Params& p, Key key, uint32_t trial, int a, int t,
+                                             const double (&rx)[3], C (&h)[NSLOT]) {
     const int S = p.n_sc;
     if constexpr (CH == CH_RAYLEIGH) {
-      const float sa = p.ant_rel[a];
+      const R sa = p.ant_rel[a];
       if (MIMO_ABL(p, ABL_RNG)) {
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s)
-          h[s] = make_float2(sa + 1e-3f * (float)((a + s + t) & 7), 0.5f - 1e-3f * (float)((a * s) & 3));
+          h[s] = mkc(sa + R(1e-3) * (R)((a + s + t) & 7), R(0.5) - R(1e-3) * (R)((a * s) & 3));
       } else {
-        normals(key, trial, ST_CHAN, (uint32_t)a, t, S, h, kNegLn2 * (sa * sa));  // ant_rel folded in
+        normals(key, trial, ST_CHAN, (uint32_t)a, t, S, h, bm_c<R>(sa * sa));  // ant_rel folded in
       }
       if constexpr (FREL) {
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s) {
           bool v;
           const int k = SL::k_of(s, t, S, v);
-          h[s] = cscale(h[s], v ? p.f_rel[k] : 0.f);
+          h[s] = cscale(h[s], v ? p.f_rel[k] : R(0));
         }
       }
     } else {
       const double tx = p.tx_pos[3 * a], ty = p.tx_pos[3 * a + 1], tz = p.tx_pos[3 * a + 2];
       const double dx = tx - rx[0], dy = ty - rx[1], dz = tz - rx[2];
       const double d_los = sqrt(dx * dx + dy * dy + dz * dz);
-      const float att_los = (float)(p.d0 / d_los);
+      const R att_los = (R)(p.d0 / d_los);
       double d_sec = 0.0;
-      float att_sec = 0.f;
+      R att_sec = R(0);
       if constexpr (CH == CH_TWOPATH) {
         // channel.py:138-147: elevation from the mirrored geometry, d_sec = tz/sin(el) +
         // rz/sin(el) with el = atan((tz + rz) / horiz), i.e. the mirrored path length
         // sqrt(horiz^2 + (tz + rz)^2) (no fp64 atan / sin; equal to ~1e-16 relative)
         const double hz = tz + rx[2];
         d_sec = sqrt(dx * dx + dy * dy + hz * hz);
-        att_sec = (float)(p.d0 / d_sec);
+        att_sec = (R)(p.d0 / d_sec);
       }
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
         bool v;
         const int k = SL::k_of(s, t, S, v);
-        float2 hv = make_float2(0.f, 0.f);
+        C hv = czero<R>();
         if (v) {
           const double foc = p.f_over_c[k];
-          const float fr = FREL ? p.f_rel[k] : 1.0f;
+          const R fr = FREL ? p.f_rel[k] : R(1);
           double ph = d_los * foc;
           ph -= floor(ph);
-          const float a1 = att_los * fr;
-          hv = make_float2(a1 * __builtin_amdgcn_cosf((float)ph), a1 * __builtin_amdgcn_sinf((float)ph));
+          const R a1 = att_los * fr;
+          hv = mkc(a1 * cos_rev((R)ph), a1 * sin_rev((R)ph));
           if constexpr (CH == CH_TWOPATH) {
             double ph2 = d_sec * foc;
             ph2 -= floor(ph2);
-            const float a2 = att_sec * fr;
-            hv.x -= a2 * __builtin_amdgcn_cosf((float)ph2);
-            hv.y -= a2 * __builtin_amdgcn_sinf((float)ph2);
+            const R a2 = att_sec * fr;
+            hv.x -= a2 * cos_rev((R)ph2);
+            hv.y -= a2 * sin_rev((R)ph2);
           }
         }
         h[s] = hv;
@@ -475,11 +501,12 @@ struct Channel {
 // allocation targets, NBUF = FFT exchange buffers (2: one barrier per exchange, 1: half
 // the LDS), SYMW_LDS = keep the pre-weighted symbols in LDS (thread-private) instead of
 // registers.  F = 2048 runs (3, 1, true): 25 KiB LDS and <= 168 VGPRs per 128-thread team.
-template <int F, int T, int NSLOT, bool ALIGNED, int CH, bool CSI, int MINW, int NBUF, bool SYMW_LDS>
-__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void trial_kernel(TrialParams p) {
-  using FFT = TeamFft<F, T, NBUF>;
+template <typename R, int F, int T, int NSLOT, bool ALIGNED, int CH, bool CSI, int MINW, int NBUF, bool SYMW_LDS>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void trial_kernel(TrialParams<R> p) {
+  using C = cx<R>;
+  using FFT = TeamFft<F, T, NBUF, R>;
   using SL = Slots<F, T, NSLOT, ALIGNED>;
-  using CHN = Channel<F, T, NSLOT, ALIGNED, CH>;
+  using CHN = Channel<R, F, T, NSLOT, ALIGNED, CH>;
   constexpr int P = FFT::P;
   constexpr int W = T / 64;
   // Without CSI errors the channel factors as H[a,k] = f_rel[k] H'[a,k]: f_rel cancels in
@@ -489,11 +516,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // mixes sub-carriers, so H keeps the factor.
   constexpr bool FREL = CSI;
 
-  __shared__ float2 lds[FFT::LDS_TOTAL];
-  __shared__ float red[kMaxWaves];
-  __shared__ float vk_part[2][kMaxWaves];
-  __shared__ float pw_csi[CSI ? kMaxCsiAnt : 1];  // per-antenna mean |H|^2 (CSI model)
-  __shared__ float2 symw_s[SYMW_LDS ? NSLOT * T : 1];  // [slot][thread]
+  __shared__ C lds[FFT::LDS_TOTAL];
+  __shared__ R red[kMaxWaves];
+  __shared__ R vk_part[2][kMaxWaves];
+  __shared__ R pw_csi[CSI ? kMaxCsiAnt : 1];  // per-antenna mean |H|^2 (CSI model)
+  __shared__ C symw_s[SYMW_LDS ? NSLOT * T : 1];  // [slot][thread]
 
   const int t = threadIdx.x;
   const bool t0 = (t == 0);
@@ -501,7 +528,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   const uint32_t trial = (uint32_t)(p.first_trial + blockIdx.x);
   const Key key{(uint32_t)p.seed, (uint32_t)(p.seed >> 32)};
   const int S = p.n_sc, A = p.n_ant, L = p.qam_l, hb = p.half_bits;
-  const float inv_sqrt_f = p.inv_sqrt_f;
+  const R inv_sqrt_f = p.inv_sqrt_f;
 
   // RX position for LoS / two-path (mp_model.py:190-201; y uses rx_loc_x, a reference quirk)
   double rx[3] = {0.0, 0.0, 0.0};
@@ -531,102 +558,102 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     valid_mask |= (v ? 1u : 0u) << s;
   }
 
-  auto frel_of = [&](int s) __attribute__((always_inline)) -> float {
+  auto frel_of = [&](int s) __attribute__((always_inline)) -> R {
     if constexpr (FREL) {
-      return 1.0f;
+      return R(1);
     } else {
       bool v;
       const int k = SL::k_of(s, t, S, v);
-      return v ? p.f_rel[k] : 1.0f;
+      return v ? p.f_rel[k] : R(1);
     }
   };
 
   // ---- pass 1: MRT norms over the (estimated) channel
-  float nrm2[NSLOT];
+  R nrm2[NSLOT];
 #pragma unroll
-  for (int s = 0; s < NSLOT; ++s) nrm2[s] = 0.f;
+  for (int s = 0; s < NSLOT; ++s) nrm2[s] = R(0);
   for (int a = 0; a < (MIMO_ABL(p, ABL_PASS1) ? 1 : A); ++a) {
     const int tl = opaque(t);
     if constexpr (CH == CH_RAYLEIGH && !CSI && MIMO_PASS1_POW) {
       if (!MIMO_ABL(p, ABL_RNG)) {
-        float e2[NSLOT];
+        R e2[NSLOT];
         CHN::power(p, key, trial, a, tl, e2);
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s) nrm2[s] += e2[s];
         continue;
       }
     }
-    float2 h[NSLOT];
+    C h[NSLOT];
     CHN::template gen<FREL>(p, key, trial, a, tl, rx, h);
     if constexpr (CSI) {
       // mp_model.py:264-282: Hhat = sqrt(1-eps^2) H + eps sqrt(mean_k |H|^2) z
-      float pw = 0.f;
+      R pw = R(0);
 #pragma unroll
-      for (int s = 0; s < NSLOT; ++s) pw = fmaf(h[s].x, h[s].x, fmaf(h[s].y, h[s].y, pw));
-      pw = team_sum<T>(pw, red) / (float)S;
+      for (int s = 0; s < NSLOT; ++s) pw = fmar(h[s].x, h[s].x, fmar(h[s].y, h[s].y, pw));
+      pw = team_sum<T>(pw, red) / (R)S;
       if (t0) pw_csi[a] = pw;
-      float2 zc[NSLOT];
+      C zc[NSLOT];
       CHN::normals(key, trial, ST_CSI, (uint32_t)a, tl, S, zc);
-      const float sc = p.csi_b * __builtin_sqrtf(pw);
+      const R sc = p.csi_b * sqrt_ieee(pw);
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s)
-        h[s] = make_float2(fmaf(p.csi_a, h[s].x, sc * zc[s].x), fmaf(p.csi_a, h[s].y, sc * zc[s].y));
+        h[s] = mkc(fmar(p.csi_a, h[s].x, sc * zc[s].x), fmar(p.csi_a, h[s].y, sc * zc[s].y));
     }
 #pragma unroll
-    for (int s = 0; s < NSLOT; ++s) nrm2[s] = fmaf(h[s].x, h[s].x, fmaf(h[s].y, h[s].y, nrm2[s]));
+    for (int s = 0; s < NSLOT; ++s) nrm2[s] = fmar(h[s].x, h[s].x, fmar(h[s].y, h[s].y, nrm2[s]));
   }
-  float inv_nrm[NSLOT];
-  float etac_p = 0.f;  // sum_k ||Hhat_k||^2 for the clean-run noise scaler (mp_model.py:304)
+  R inv_nrm[NSLOT];
+  R etac_p = R(0);  // sum_k ||Hhat_k||^2 for the clean-run noise scaler (mp_model.py:304)
 #pragma unroll
   for (int s = 0; s < NSLOT; ++s) {
     const bool v = (valid_mask >> s) & 1u;
-    inv_nrm[s] = v ? __builtin_amdgcn_rsqf(nrm2[s]) : 0.f;
-    const float fr = frel_of(s);
-    etac_p += v ? nrm2[s] * (fr * fr) : 0.f;
+    inv_nrm[s] = v ? rsq_r(nrm2[s]) : R(0);
+    const R fr = frel_of(s);
+    etac_p += v ? nrm2[s] * (fr * fr) : R(0);
   }
   if constexpr (CSI) __syncthreads();  // pw_csi visible
 
-  float2 d[P];
-  float2 r[NSLOT];
-  float g[NSLOT];
-  float2 cc[CSI ? NSLOT : 1];  // clean-run combine sum_a H conj(Hhat)/||Hhat|| (CSI only)
+  C d[P];
+  C r[NSLOT];
+  R g[NSLOT];
+  C cc[CSI ? NSLOT : 1];  // clean-run combine sum_a H conj(Hhat)/||Hhat|| (CSI only)
 #pragma unroll
   for (int s = 0; s < NSLOT; ++s) {
-    r[s] = make_float2(0.f, 0.f);
-    g[s] = 0.f;
-    if constexpr (CSI) cc[s] = make_float2(0.f, 0.f);
+    r[s] = czero<R>();
+    g[s] = R(0);
+    if constexpr (CSI) cc[s] = czero<R>();
   }
 
   // ---- array pass: precode -> IFFT -> PA -> FFT -> combine, one antenna at a time.
   // MAIN: symbols = tx labels, combine with the true channel, accumulate g (alpha_a).
   // MCNC: symbols = detected labels, combine with the estimated channel (corrector.py:198-200).
   // The symbols enter pre-weighted, symw = s / ||Hhat|| / sqrt(F) (0 on invalid slots).
-  float2 symw_r[SYMW_LDS ? 1 : NSLOT];
+  C symw_r[SYMW_LDS ? 1 : NSLOT];
   auto set_symbols = [&](const uint32_t (&lab_in)[NSLOT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
-      const float2 v = cscale(qam_point(lab_in[s], L, hb), inv_nrm[s] * inv_sqrt_f);
+      const C v = cscale(qam_point<R>(lab_in[s], L, hb), inv_nrm[s] * inv_sqrt_f);
       if constexpr (SYMW_LDS) symw_s[s * T + t] = v; else symw_r[s] = v;
     }
   };
-  auto symw = [&](int s) __attribute__((always_inline)) -> float2 {
+  auto symw = [&](int s) __attribute__((always_inline)) -> C {
     if constexpr (SYMW_LDS) return symw_s[s * T + t]; else return symw_r[s];
   };
-  auto array_pass = [&](bool main_pass, float2 (&acc)[NSLOT]) __attribute__((always_inline)) {
+  auto array_pass = [&](bool main_pass, C (&acc)[NSLOT]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int s = 0; s < NSLOT; ++s) acc[s] = make_float2(0.f, 0.f);
+    for (int s = 0; s < NSLOT; ++s) acc[s] = czero<R>();
     // Software pipeline (PIPE): antenna a+1's channel draws (one Philox call per chunk)
     // run inside antenna a's FFT exchanges, where the wave otherwise waits on LDS.
     constexpr bool PIPE = MIMO_HPIPE && ALIGNED && CH == CH_RAYLEIGH && !CSI;
-    float2 hnext[PIPE ? NSLOT : 1];
+    C hnext[PIPE ? NSLOT : 1];
     if constexpr (PIPE) {
-      const float sa = p.ant_rel[0];
+      const R sa = p.ant_rel[0];
       if (MIMO_ABL(p, ABL_RNG)) CHN::template gen<FREL>(p, key, trial, 0, t, rx, hnext);
-      else CHN::normals(key, trial, ST_CHAN, 0u, t, S, hnext, kNegLn2 * (sa * sa));
+      else CHN::normals(key, trial, ST_CHAN, 0u, t, S, hnext, bm_c<R>(sa * sa));
     }
     for (int a = 0; a < A; ++a) {
       const int tl = opaque(t);
-      float2 h[NSLOT];
+      C h[NSLOT];
       if constexpr (PIPE) {
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s) h[s] = hnext[s];
@@ -634,7 +661,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         CHN::template gen<FREL>(p, key, trial, a, tl, rx, h);
       }
       const int an = a + 1 < A ? a + 1 : a;  // the last antenna redraws itself (unused)
-      const float san = PIPE ? p.ant_rel[an] : 0.f;
+      const R san = PIPE ? p.ant_rel[an] : R(0);
       // Window w of NW = 2 XCHG exchange windows (IFFT then FFT) draws chunks
       // [w NC / NW, (w + 1) NC / NW) of antenna a+1.
       auto hfill = [&](int w) __attribute__((always_inline)) {
@@ -644,33 +671,33 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 #pragma unroll
             for (int c = 0; c < NC; ++c)
               if (c >= w * NC / NW && c < (w + 1) * NC / NW)
-                CHN::normals_chunk(c, key, trial, ST_CHAN, (uint32_t)an, tl, S, hnext, kNegLn2 * (san * san));
+                CHN::normals_chunk(c, key, trial, ST_CHAN, (uint32_t)an, tl, S, hnext, bm_c<R>(san * san));
           }
         }
       };
       auto hfill_ifft = [&](int w) __attribute__((always_inline)) { hfill(w); };
       auto hfill_fft = [&](int w) __attribute__((always_inline)) { hfill(FFT::XCHG + w); };
-      float2 he[CSI ? NSLOT : 1];
+      C he[CSI ? NSLOT : 1];
       if constexpr (CSI) {
-        float2 zc[NSLOT];
+        C zc[NSLOT];
         CHN::normals(key, trial, ST_CSI, (uint32_t)a, tl, S, zc);
-        const float sc = p.csi_b * __builtin_sqrtf(pw_csi[a]);
+        const R sc = p.csi_b * sqrt_ieee(pw_csi[a]);
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s)
-          he[s] = make_float2(fmaf(p.csi_a, h[s].x, sc * zc[s].x), fmaf(p.csi_a, h[s].y, sc * zc[s].y));
+          he[s] = mkc(fmar(p.csi_a, h[s].x, sc * zc[s].x), fmar(p.csi_a, h[s].y, sc * zc[s].y));
       }
-      auto hest = [&](int s) __attribute__((always_inline)) -> float2 {
+      auto hest = [&](int s) __attribute__((always_inline)) -> C {
         if constexpr (CSI) return he[s]; else return h[s];
       };
-      float2 x[NSLOT];
-      float e2[NSLOT];  // |Hhat|^2, kept for g after the FFT
-      float vk = 0.f;
+      C x[NSLOT];
+      R e2[NSLOT];  // |Hhat|^2, kept for g after the FFT
+      R vk = R(0);
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
-        const float2 e = hest(s);
+        const C e = hest(s);
         x[s] = cmulc(symw(s), e);  // s conj(Hhat) / ||Hhat|| / sqrt(F); 0 off band (symw = 0)
-        e2[s] = fmaf(e.x, e.x, e.y * e.y);
-        vk = fmaf(e2[s], inv_nrm[s] * inv_nrm[s], vk);  // inv_nrm = 0 off band
+        e2[s] = fmar(e.x, e.x, e.y * e.y);
+        vk = fmar(e2[s], inv_nrm[s] * inv_nrm[s], vk);  // inv_nrm = 0 off band
       }
       if (main_pass) {
 #if MIMO_VK_DPP
@@ -693,18 +720,18 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         }
       }
       if (MIMO_ABL(p, ABL_FFT)) __syncthreads();  // keep the vk_part hand-off ordered
-      float alpha_a = 0.f;
+      R alpha_a = R(0);
       if (main_pass) {
-        float vks = 0.f;
+        R vks = R(0);
 #pragma unroll
         for (int i = 0; i < W; ++i) vks += vk_part[a & 1][i];
-        const float x = fmaf(vks, p.inv_vk0, -1.0f);
+        const R x = fmar(vks, p.inv_vk0, -R(1));
         // Polynomial alpha: -7 % at F = 2048, but +3 % at F = 8192 (SGPR pressure of the
         // 8 waves/team instance, tools/ab_libs.py), so only up to F = 4096.
-        if (MIMO_ALPHA_POLY && F <= 4096 && fabsf(x) <= p.alpha_xlim) {
-          float acc = p.apoly[8];
+        if (MIMO_ALPHA_POLY && sizeof(R) == 4 && F <= 4096 && absr(x) <= p.alpha_xlim) {
+          R acc = p.apoly[8];
 #pragma unroll
-          for (int i = 7; i >= 0; --i) acc = fmaf(acc, x, p.apoly[i]);
+          for (int i = 7; i >= 0; --i) acc = fmar(acc, x, p.apoly[i]);
           alpha_a = acc;
         } else {
           alpha_a = alpha_of_gamma2(p.alpha_c / vks);
@@ -712,11 +739,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       }
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
-        const float2 y = SL::gather(d, s, t0);
+        const C y = SL::gather(d, s, t0);
         if (main_pass) {
           acc[s] = cmac(acc[s], h[s], y);
-          g[s] = fmaf(alpha_a, e2[s], g[s]);  // sum_a alpha_a |Hhat|^2; x 1/||Hhat|| after the pass
-          const float2 e = hest(s);
+          g[s] = fmar(alpha_a, e2[s], g[s]);  // sum_a alpha_a |Hhat|^2; x 1/||Hhat|| after the pass
+          const C e = hest(s);
           if constexpr (CSI) cc[s] = cadd(cc[s], cscale(cmulc(h[s], e), inv_nrm[s]));
         } else {
           acc[s] = cmac(acc[s], hest(s), y);
@@ -739,54 +766,54 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   gen_labels(opaque(t), lab);
 
   // ---- AWGN + AGC (noise.py:56-83 on all bins; only in-band bins matter)
-  float2 zn[NSLOT];
+  C zn[NSLOT];
   CHN::normals(key, trial, ST_NOISE, 0u, t, S, zn);
-  float eta_p = 0.f;
+  R eta_p = R(0);
 #pragma unroll
   for (int s = 0; s < NSLOT; ++s) {
-    const float gs = g[s] * frel_of(s);
-    eta_p = ((valid_mask >> s) & 1u) ? fmaf(gs, gs, eta_p) : eta_p;
+    const R gs = g[s] * frel_of(s);
+    eta_p = ((valid_mask >> s) & 1u) ? fmar(gs, gs, eta_p) : eta_p;
   }
-  const float eta = team_sum<T>(eta_p, red) / (float)S;
+  const R eta = team_sum<T>(eta_p, red) / (R)S;
   uint32_t* out = p.counts + (size_t)blockIdx.x * p.n_idx;
 
   auto record = [&](int idx, uint32_t errs) __attribute__((always_inline)) {
-    const float tot = team_sum<T>((float)errs, red);
-    if (t0) out[idx] = (uint32_t)(tot + 0.5f);
+    const R tot = team_sum<T>((R)errs, red);
+    if (t0) out[idx] = (uint32_t)(tot + R(0.5));
   };
 
   if (p.incl_clean) {
     // clean run (mp_model.py:159-175): no PA, AGC / noise from sum_a Hhat P = ||Hhat||
-    const float etac = team_sum<T>(etac_p, red) / (float)S;
-    const float sig_c = __builtin_sqrtf(p.es_over_snr * etac);
+    const R etac = team_sum<T>(etac_p, red) / (R)S;
+    const R sig_c = sqrt_ieee(p.es_over_snr * etac);
     uint32_t errs = 0;
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
-      const float2 sym = qam_point(lab[s], L, hb);
-      float2 rc;
-      if constexpr (CSI) rc = cmul(cc[s], sym); else rc = cscale(sym, inv_nrm[s] > 0.f ? 1.0f / inv_nrm[s] : 0.f);
-      const float ig = inv_nrm[s];  // 1 / ||Hhat||  (/ f_rel when factored)
-      const float sn = sig_c / frel_of(s);
-      const float2 zc = make_float2((rc.x + sn * zn[s].x) * ig, (rc.y + sn * zn[s].y) * ig);
+      const C sym = qam_point<R>(lab[s], L, hb);
+      C rc;
+      if constexpr (CSI) rc = cmul(cc[s], sym); else rc = cscale(sym, inv_nrm[s] > R(0) ? R(1) / inv_nrm[s] : R(0));
+      const R ig = inv_nrm[s];  // 1 / ||Hhat||  (/ f_rel when factored)
+      const R sn = sig_c / frel_of(s);
+      const C zc = mkc((rc.x + sn * zn[s].x) * ig, (rc.y + sn * zn[s].y) * ig);
       const uint32_t lh = slice(zc, L, hb);
       errs += ((valid_mask >> s) & 1u) ? __popc(lh ^ lab[s]) : 0u;
     }
     record(0, errs);
   }
 
-  const float sig = __builtin_sqrtf(p.es_over_snr * eta);
-  float2 z[NSLOT];
+  const R sig = sqrt_ieee(p.es_over_snr * eta);
+  C z[NSLOT];
 #pragma unroll
   for (int s = 0; s < NSLOT; ++s) {
-    const float ig = ((valid_mask >> s) & 1u) ? 1.0f / g[s] : 0.f;
-    const float sn = sig / frel_of(s);
-    z[s] = make_float2((r[s].x + sn * zn[s].x) * ig, (r[s].y + sn * zn[s].y) * ig);
+    const R ig = ((valid_mask >> s) & 1u) ? R(1) / g[s] : R(0);
+    const R sn = sig / frel_of(s);
+    z[s] = mkc((r[s].x + sn * zn[s].x) * ig, (r[s].y + sn * zn[s].y) * ig);
   }
 
   // ---- CNC / MCNC receiver
-  float2 dist[NSLOT];
+  C dist[NSLOT];
 #pragma unroll
-  for (int s = 0; s < NSLOT; ++s) dist[s] = make_float2(0.f, 0.f);
+  for (int s = 0; s < NSLOT; ++s) dist[s] = czero<R>();
   int idx = p.incl_clean;
   for (int it = 0; it <= p.max_iter; ++it) {
     uint32_t lh[NSLOT];
@@ -800,29 +827,29 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     if (it == p.max_iter) break;
     if (p.receiver == RX_CNC) {
       // corrector.py:84-110: single-antenna re-synthesis of the clipping distortion
-      float2 x[NSLOT];
+      C x[NSLOT];
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s)
-        x[s] = ((valid_mask >> s) & 1u) ? cscale(qam_point(lh[s], L, hb), inv_sqrt_f) : make_float2(0.f, 0.f);
+        x[s] = ((valid_mask >> s) & 1u) ? cscale(qam_point<R>(lh[s], L, hb), inv_sqrt_f) : czero<R>();
       SL::scatter(d, x, t0);
       FFT::template run<+1, 0, SL::zero_mask()>(d, lds, p.tw, t);
       pa_block(p.cnc_pa_kind, d, p.sat_cnc, p.sqrt_sat_cnc, p.inv_sat_cnc, p.rapp_p, p.toi_cnc);
       FFT::template run_second<-1>(d, lds, p.tw, t);
-      const float sc = inv_sqrt_f * p.inv_alpha_cnc;
+      const R sc = inv_sqrt_f * p.inv_alpha_cnc;
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
-        const float2 y = SL::gather(d, s, t0);
-        dist[s] = ((valid_mask >> s) & 1u) ? csub(cscale(y, sc), qam_point(lh[s], L, hb)) : make_float2(0.f, 0.f);
+        const C y = SL::gather(d, s, t0);
+        dist[s] = ((valid_mask >> s) & 1u) ? csub(cscale(y, sc), qam_point<R>(lh[s], L, hb)) : czero<R>();
       }
     } else {
-      float2 est[NSLOT];
+      C est[NSLOT];
       set_symbols(lh);
       array_pass(false, est);
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
-        const float ig = ((valid_mask >> s) & 1u) ? 1.0f / g[s] : 0.f;
-        dist[s] = ((valid_mask >> s) & 1u) ? csub(cscale(est[s], ig), qam_point(lh[s], L, hb))
-                                           : make_float2(0.f, 0.f);
+        const R ig = ((valid_mask >> s) & 1u) ? R(1) / g[s] : R(0);
+        dist[s] = ((valid_mask >> s) & 1u) ? csub(cscale(est[s], ig), qam_point<R>(lh[s], L, hb))
+                                           : czero<R>();
       }
     }
   }

@@ -8,6 +8,11 @@ namespace mimo {
 
 // Team (workgroup) size per FFT size: 16 points per thread from F = 1024 up, one wave below.
 constexpr int team_size(int F) { return F >= 1024 ? F / 16 : 64; }
+// fp64 instances: 8 points per thread from F = 512 up (a complex double takes 4 VGPRs,
+// so P = 8 holds the same 32 data registers as the fp32 team's P = 16), one wave below.
+// F = 8192: 16 points per thread (a 1024-thread team would cap the waves at 128 VGPRs;
+// its one 136 KiB exchange buffer allows one team per CU either way).
+constexpr int team_size64(int F) { return F >= 8192 ? F / 16 : F >= 512 ? F / 8 : 64; }
 // Alternative team (8 points per thread: half the registers, 2x the waves, one more
 // LDS exchange per transform), selectable with MIMO_TEAM=<T> for A/B measurements.
 constexpr int alt_team_size(int F) { return F >= 1024 ? F / 8 : team_size(F); }
@@ -17,11 +22,14 @@ struct InstanceKey {
   bool aligned;
   int ch;
   bool csi;
+  bool f64;  // arithmetic type of the instance (TrialParams<double>)
 };
 
-#define MIMO_DECLARE_LAUNCH(FV)                                                                  \
-  hipError_t launch_trial_F##FV(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams& p, \
-                                bool* found);
+#define MIMO_DECLARE_LAUNCH(FV)                                                                           \
+  hipError_t launch_trial_F##FV##_f32(const InstanceKey& k, dim3 grid, hipStream_t st,                    \
+                                      const TrialParams<float>& p, bool* found);                          \
+  hipError_t launch_trial_F##FV##_f64(const InstanceKey& k, dim3 grid, hipStream_t st,                    \
+                                      const TrialParams<double>& p, bool* found);
 MIMO_DECLARE_LAUNCH(128)
 MIMO_DECLARE_LAUNCH(256)
 MIMO_DECLARE_LAUNCH(512)

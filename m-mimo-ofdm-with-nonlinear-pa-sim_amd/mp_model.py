@@ -56,7 +56,7 @@ class Link:
 
     def __init__(self, mod_obj: OfdmQamModem, array_obj: AntennaArray, std_rx_obj: Transceiver, chan_obj, noise_obj,
                  rx_loc_var: float, n_err_min: int, bits_sent_max: int, is_mcnc: bool = False,
-                 csi_epsylon: float = None, device: int = None, max_batch: int = MAX_BATCH):
+                 csi_epsylon: float = None, device: int = None, max_batch: int = MAX_BATCH, precision: str = None):
         self.my_mod = copy.deepcopy(mod_obj)
         self.my_array = copy.deepcopy(array_obj)
         self.my_standard_rx = copy.deepcopy(std_rx_obj)
@@ -89,6 +89,7 @@ class Link:
         self.n_err_min = n_err_min
         self.bits_sent_max = bits_sent_max
         self.device = device
+        self.precision = precision  # "f64" (default: the reference's float64) or "f32"
         self.max_batch = int(max_batch)
         self._engine = None
         self._engine_key = None
@@ -109,7 +110,7 @@ class Link:
             raise NotImplementedError("a fixed Rayleigh realisation (reroll_chan=False) is not supported: "
                                       "the engine draws every trial's channel on the device")
         dev = self.device if self.device is not None else _default_device()
-        key = (dev, kind, bool(reroll_chan), self.is_mcnc)
+        key = (dev, kind, bool(reroll_chan), self.is_mcnc, self.precision)
         if self._engine is None or self._engine_key != key:
             m = self.my_mod
             rx = self.my_standard_rx
@@ -119,7 +120,8 @@ class Link:
                 self.n_ant_val, m.n_sub_carr, m.n_fft, m.constel_size, m.cp_len, kind,
                 "mcnc" if self.is_mcnc else "cnc", self.my_array.positions(),
                 (self.rx_loc_x, self.rx_loc_y, rx.cord_z), self.rx_loc_var,
-                channel.carrier_freqs(m.n_fft, rx.carrier_spacing, rx.center_freq), reroll=reroll_chan, device=dev)
+                channel.carrier_freqs(m.n_fft, rx.carrier_spacing, rx.center_freq), reroll=reroll_chan, device=dev,
+                precision=self.precision)
             self._engine_key = key
         self._push_point()
         return self._engine

@@ -5,11 +5,14 @@ from oracle import refmath as rm
 from oracle.sim import SimConfig, point_params
 
 
-def engine_for(cfg: SimConfig, device=-1):
+PRECISIONS = ["f64", "f32"]  # every parity test runs both instances of the fused kernel
+
+
+def engine_for(cfg: SimConfig, device=-1, precision=None):
     import _engine
     carriers = rm.fftfreq_carriers(cfg.n_fft, cfg.carrier_spacing, cfg.center_freq)
     eng = _engine.Engine(cfg.n_ant, cfg.n_sc, cfg.n_fft, cfg.constel_size, 4, cfg.channel, cfg.receiver, cfg.tx_pos,
-                         cfg.rx_pos, cfg.rx_loc_var, carriers, reroll=cfg.reroll, device=device)
+                         cfg.rx_pos, cfg.rx_loc_var, carriers, reroll=cfg.reroll, device=device, precision=precision)
     pp = point_params(cfg)
     avg = pp["avg_samp"] / cfg.n_ant  # MRT: mean |P|^2 = 1/A (antenna_array.py:328-335)
     if cfg.pa == "toi":
@@ -20,6 +23,17 @@ def engine_for(cfg: SimConfig, device=-1):
                   cnc_sat_pow=pp["cnc_sat"], cnc_toi_coeff=pp["cnc_coeff"], cnc_alpha=pp["cnc_alpha"],
                   csi_eps=cfg.csi_eps, **kw)
     return eng
+
+
+def assert_counts_equal(per, ref, label=""):
+    """Per-trial, per-iteration bit-error counts must agree EXACTLY (both kernels, both
+    precisions: the device sees the oracle's Philox draws, so only a received point
+    within rounding distance of a slicer boundary could flip; none does on these cases)."""
+    per = np.asarray(per, np.int64)
+    ref = np.asarray(ref, np.int64)
+    assert per.shape == ref.shape, (per.shape, ref.shape)
+    bad = np.argwhere(per != ref)
+    assert bad.size == 0, f"{label}: {len(bad)} of {per.size} entries differ, first {bad[:5].tolist()}"
 
 
 def count_agreement(a, b):

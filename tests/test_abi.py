@@ -30,14 +30,14 @@ def test_library_exports_every_declared_symbol():
     lib = _engine.lib()
     missing = [n for n in declared_functions() if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.mimo_abi_version() == 1
+    assert lib.mimo_abi_version() == 2
 
 
 def _cfg(**kw):
     tx = np.zeros((kw.get("n_ant", 4), 3))
     fr = np.full(kw.get("n_fft", 256), 3.5e9)
     base = dict(n_ant=4, n_sub_carr=128, n_fft=256, constel_size=16, cp_len=16, channel_kind=1, receiver_kind=1,
-                device=-1, rx_loc_var=10.0, reroll_chan=1, reserved=0)
+                device=-1, rx_loc_var=10.0, reroll_chan=1, precision=0)
     base.update(kw)
     c = _engine.MimoConfig(**base, tx_pos=tx.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
                            carrier_freqs=fr.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
@@ -54,6 +54,7 @@ def _cfg(**kw):
     (dict(n_ant=0), "n_ant must be in"),
     (dict(channel_kind=7), "unknown channel_kind"),
     (dict(receiver_kind=0), "unknown receiver_kind"),
+    (dict(precision=2), "precision must be"),
 ])
 def test_create_rejects_invalid_configs(kw, msg):
     lib = _engine.lib()
@@ -74,7 +75,7 @@ def test_valid_engine_is_host_only_until_run():
                            csi_eps=-1.0)
     assert lib.mimo_engine_set_point(h, ctypes.byref(pt)) == 0
     desc = lib.mimo_engine_describe(h).decode()
-    assert "F=512" in desc and "aligned" in desc, desc
+    assert "F=512" in desc and "aligned" in desc and desc.endswith("f64"), desc
     bad = _engine.MimoPoint(**{f: getattr(pt, f) for f, _ in _engine.MimoPoint._fields_})
     bad.csi_eps = 1.5
     assert lib.mimo_engine_set_point(h, ctypes.byref(bad)) == -1  # MIMO_EINVAL
@@ -126,3 +127,16 @@ def test_run_validates_arguments_before_any_hip_call(iters, first, n, msg):
     assert rc == -1 and "set_point" in lib.mimo_last_error().decode()
     lib.mimo_engine_destroy(h)
     lib.mimo_engine_destroy(h2)
+
+
+@pytest.mark.parametrize("prec,team", [(0, 64), (1, 64)])
+def test_precision_selects_the_instance(prec, team):
+    """precision = MIMO_PREC_F64 (default 0: the reference's float64) or MIMO_PREC_F32."""
+    lib = _engine.lib()
+    c, keep = _cfg(n_fft=2048, n_sub_carr=1024, precision=prec)
+    h = lib.mimo_engine_create(ctypes.byref(c))
+    desc = lib.mimo_engine_describe(h).decode()
+    # fp64 teams hold 8 points per thread (T = F/8), fp32 teams 16 (T = F/16)
+    assert desc.startswith("F=2048 T=256" if prec == 0 else "F=2048 T=128"), desc
+    assert desc.endswith("f64" if prec == 0 else "f32"), desc
+    lib.mimo_engine_destroy(h)

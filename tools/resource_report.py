@@ -23,12 +23,12 @@ for line in out.splitlines():
         name = s.split(":", 1)[1].strip()
         t = re.search(r"trial_kernelI(.*)EEvNS", name)
         args = re.findall(r"L([ib])(\d+)E", t.group(1)) if t else []
-        cur = {"inst": ",".join(v for _, v in args)}
+        cur = {"inst": ("f64," if "trial_kernelId" in name else "f32,") + ",".join(v for _, v in args)}
         rows.append(cur)
     elif cur is not None and ":" in s:
         k, v = s.split(":", 1)
         cur[k.strip()] = v.strip()
-print("F,T,NSLOT,aligned,CH,CSI,MINW,NBUF,SYMW_LDS  VGPRs spill occ LDS")
+print("R,F,T,NSLOT,aligned,CH,CSI,MINW,NBUF,SYMW_LDS  VGPRs spill occ LDS")
 for r in rows:
     print(f'{r["inst"]:34s} {r.get("VGPRs","?"):>4} {r.get("VGPRs Spill","?"):>4} {r.get("Occupancy [waves/SIMD]","?"):>3} '
           f'{r.get("LDS Size [bytes/block]","?")}')
