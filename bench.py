@@ -55,7 +55,10 @@ WORKLOADS = {
 A, S, F, M, CP = 64, 1024, 2048, 64, 128
 IBO, EBN0 = 3.0, 15.0
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-FP32_PEAK_TFLOPS = 157.3   # gfx950 dense FP32 (MFMA f32 == VALU f32 peak)
+# Dense vector peaks of the arithmetic type the kernel computes in.  f32: MI355X_MICROARCH.md
+# (157.3 TF, VALU == MFMA f32).  f64: AMD's MI355X spec sheet (78.6 TF vector; the guide
+# lists no f64 figure) -- the fused kernel issues no MFMA, so the VALU peak is the ceiling.
+VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}
 
 
 def bytes_alg_per_trial(a=A, s=S, f=F):
@@ -107,39 +110,81 @@ def make_engine(device, workload="2", precision="f64"):
     return link.engine()
 
 
-def cpu_baseline(seconds=15.0, workload="2", iters=(0,)):
-    """The float64 oracle (oracle/sim.py, NumPy, one process / one core) on a bounded sample
-    of the same workload (same receiver iterations): reported beside the GPU number, never
-    the measured product."""
+def _cpu_worker(args):
+    """One host process of the CPU baseline: trials of the workload through oracle/sim.py for
+    ``seconds`` of wall time; returns the number of trials it finished."""
+    workload, iters, seconds, wid = args
     from oracle import refmath as rm
     from oracle.sim import SimConfig, run_trials
     w = WORKLOADS[workload]
     cfg = SimConfig(w["A"], w["S"], w["F"], w["M"], pa=w["pa"], p_hardness=w["p"], ibo_db=w["ibo"],
                     snr_db=float(rm.ebn0_to_snr(w["ebn0"], w["S"], w["S"], w["M"])), channel=w.get("chan", "rayleigh"),
                     receiver="mcnc" if w.get("mcnc") else "cnc", csi_eps=w.get("csi"))
-    iters = list(iters)
-    run_trials(cfg, 7, [0], iters=iters)  # warm caches / imports
-    n, t0 = 0, time.perf_counter()
+    step = 4 if w["F"] <= 2048 else 1
+    run_trials(cfg, 7, [0], iters=list(iters))  # warm caches / imports
+    n, base, t0 = 0, (wid + 1) << 24, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        step = 16 if w["F"] <= 2048 else 2
-        run_trials(cfg, 7, np.arange(n, n + step), iters=iters)
+        run_trials(cfg, 7, np.arange(base + n, base + n + step), iters=list(iters))
         n += step
-    dt = time.perf_counter() - t0
-    rx = "standard RX" if iters == [0] else f"receiver iterations {iters}"
-    return dict(value=round(n / dt, 3), unit="OFDM symbols/s", cores=1, kind="port",
-                sample=f"{n} trials of the workload-{workload} chain ({rx}) through oracle/sim.py "
-                       f"(NumPy float64, 1 process, {dt:.1f} s)")
+    return n, time.perf_counter() - t0
 
 
-def load_pmc_traffic(trials_per_launch):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if one matches."""
+def cpu_cores():
+    """Host cores the baseline may use: this process's CPU affinity, capped at 16 (a GPU
+    box's share per GPU; its nproc shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_baseline(seconds=15.0, workload="2", iters=(0,), cores=None):
+    """The float64 oracle (oracle/sim.py, NumPy) fanned out over the host's cores the way the
+    reference's drivers fan ``Link.simulate`` out (``mp.Process`` x cores,
+    main_mp_miso_cnc_ber_vs_ebn0.py:122-132), on a bounded sample of the same workload (same
+    receiver iterations).  Reported beside the GPU number, never the measured product.
+    Workers are spawned (fresh interpreters, one NumPy thread each), not forked from a process
+    that holds a HIP context."""
+    import multiprocessing as mp
+    cores = cores or cpu_cores()
+    iters = list(iters)
+    env_keys = ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")
+    saved = {k: os.environ.get(k) for k in env_keys}
+    for k in env_keys:
+        os.environ[k] = "1"
+    try:
+        ctx = mp.get_context("spawn")
+        t0 = time.perf_counter()
+        with ctx.Pool(cores) as pool:
+            res = pool.map(_cpu_worker, [(workload, tuple(iters), seconds, i) for i in range(cores)])
+        wall = time.perf_counter() - t0
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    n = sum(r[0] for r in res)
+    busy = max(r[1] for r in res)
+    w = WORKLOADS[workload]
+    rx = ("MCNC" if w.get("mcnc") else "CNC") + f" iterations {iters}" if iters != [0] else "standard RX"
+    return dict(value=round(n / busy, 3), unit="OFDM symbols/s", cores=cores, kind="port",
+                sample=f"{n} trials of the workload-{workload} chain ({rx}) through oracle/sim.py (NumPy float64), "
+                       f"{cores} spawned processes x {busy:.1f} s each (pool wall {wall:.1f} s incl. start-up)")
+
+
+def load_pmc_traffic(workload, iters, precision, trials_per_launch):
+    """Per-launch HBM bytes from a committed rocprofv3 PMC summary of the SAME workload,
+    receiver iterations, precision and batch (tools/pmc_summary.py writes them)."""
+    key = dict(workload=workload, iters=list(iters), precision=precision, trials_per_launch=trials_per_launch)
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "*pmc*.json"), recursive=True), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if d.get("trials_per_launch") == trials_per_launch and "hbm_bytes_per_launch" in d:
+        if all(d.get(k) == v for k, v in key.items()) and "hbm_bytes_per_launch" in d:
             return d["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
     return None, None
 
@@ -213,7 +258,10 @@ def main():
     b_alg = bytes_alg_per_trial(wl["A"], wl["S"], wl["F"]) * B
     f_trial = flops_alg_per_trial(wl["A"], wl["S"], wl["F"], max(iters), wl.get("mcnc", False))
     f_alg = f_trial * B
-    traffic, traffic_src = load_pmc_traffic(B) if args.workload == "2" else (None, None)
+    traffic, traffic_src = load_pmc_traffic(args.workload, iters, args.precision, B)
+    peak = VALU_PEAK_TFLOPS[args.precision]
+    achieved = f_alg / avg_kernel_s / 1e12
+    rx = "standard RX" if iters == [0] else ("MCNC" if wl.get("mcnc") else "CNC") + f" iterations {iters}"
     out = {
         "metric": "OFDM symbols/s/GPU (64-ant,1024-sc) + achieved HBM %peak; BER match vs ref",
         "value": round(value, 1),
@@ -227,20 +275,25 @@ def main():
         "vs_baseline": None,
         "dtype": args.precision,
         "data": "synthetic (on-device Philox bits / Rayleigh channel / AWGN)",
-        "config": {"workload": wl["desc"] + (", standard RX" if iters == [0] else f", CNC iterations {iters}"),
+        "config": {"workload": wl["desc"] + ", " + rx,
                    "trials_per_gpu_per_step": B, "iters": iters, "parallelism": f"trial-sharded x{world}"},
         "roofline": {
-            "bound": "mfma", "regime": "fp32 VALU (gfx950 f32 MFMA peak == f32 VALU peak)",
-            "achieved": round(f_alg / avg_kernel_s / 1e12, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(f_alg / avg_kernel_s / 1e12 / FP32_PEAK_TFLOPS, 4),
+            "bound": "valu", "regime": f"{args.precision} VALU issue (fused kernel, no MFMA-shaped work at one user)",
+            "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": traffic, "traffic_source": traffic_src,
             "kernel": "mimo::trial_kernel " + eng.describe(), "kernel_ms": round(avg_kernel_s * 1e3, 3),
-            "flops_alg_per_trial": f_trial,
+            "flops_alg_per_trial": f_trial, "trials_per_launch": B,
         },
-        "hbm_alg": {"achieved": round(b_alg / avg_kernel_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(b_alg / avg_kernel_s / 1e9 / HBM_PEAK_GBS, 4),
-                    "bytes_alg_per_trial": bytes_alg_per_trial(wl["A"], wl["S"], wl["F"]),
-                    "note": "SURVEY §8(d) staged-pipeline bytes; the fused kernel keeps them on chip"},
+        # BASELINE's "achieved HBM %peak": the fused kernel keeps SURVEY §8(d)'s staged-pipeline
+        # bytes on chip, so the HBM fraction is the MEASURED traffic (PMC, when a matching
+        # summary exists) over the kernel time -- not the staged model's bytes.
+        "hbm": {"measured_GBps": None if traffic is None else round(traffic / avg_kernel_s / 1e9, 2),
+                "measured_frac": None if traffic is None else round(traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS, 5),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "staged_model_bytes_per_trial": bytes_alg_per_trial(wl["A"], wl["S"], wl["F"]),
+                "staged_model_equiv_GBps": round(b_alg / avg_kernel_s / 1e9, 1),
+                "note": "staged_model_* = SURVEY §8(d) K1-K4 bytes a staged pipeline would move for the same "
+                        "trials; the fused kernel does not move them (a model figure, not traffic)"},
         "ber": [round(float(x) / (total_trials * wl["S"] * np.log2(wl["M"])), 8) for x in err_tot],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
