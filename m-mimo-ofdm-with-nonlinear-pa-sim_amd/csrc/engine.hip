@@ -91,6 +91,33 @@ void fit_alpha(double g0sq, P& p) {
   p.alpha_xlim = (R)L;
 }
 
+// fp64 Box-Muller tables (real.h ln_lut / sincos_lut), computed in long double.
+std::vector<double2> lut64_table() {
+  std::vector<double2> t(mimo::kLut64);
+  for (int i = 0; i < mimo::kLnTab; ++i) {
+    // bucket i: high word 0x3FE00000 | (i & 255) << 12 (i < 256) or 0x3FF00000 | ... (i >= 256)
+    const bool one = i >= 256;
+    const int j = i & 255;
+    const long double lo = one ? 1.0L + j / 256.0L : 0.5L + j / 512.0L;
+    const long double w = one ? 1.0L / 256 : 1.0L / 512;
+    double c;
+    if ((one && j == 0) || (!one && j == 255)) {
+      c = 1.0;  // the buckets next to 1: t = m - 1 exactly
+    } else {
+      const long double ctr = lo + 0.5L * w;
+      int ex;
+      const long double fr = std::frexp(1.0L / ctr, &ex);       // [0.5, 1)
+      c = (double)std::ldexp(std::round(std::ldexp(fr, 12)), ex - 12);  // 12 significant bits
+    }
+    t[i] = make_double2(c, (double)(-std::log((long double)c)));
+  }
+  for (int i = 0; i < mimo::kScTab; ++i) {
+    const long double a = 2.0L * 3.14159265358979323846264338327950288L * i / mimo::kScTab;
+    t[mimo::kLnTab + i] = make_double2((double)std::cos(a), (double)std::sin(a));
+  }
+  return t;
+}
+
 }  // namespace
 
 namespace mimo {
@@ -109,6 +136,7 @@ struct mimo_engine {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float2* d_tw[2] = {nullptr, nullptr};  // fp32 stage twiddles for team_size(F), alt_team_size(F)
   double2* d_tw64 = nullptr;              // fp64 stage twiddles for team_size64(F)
+  double2* d_lut64 = nullptr;             // fp64 Box-Muller tables (lut64_table)
   float* d_ant_rel = nullptr;
   float* d_f_rel = nullptr;
   double* d_ant_rel64 = nullptr;
@@ -276,6 +304,9 @@ int ensure_device(mimo_engine* e) {
     HIP_TRY(hipMalloc(&e->d_tw[v], sizeof(float2) * tws[v].size()));
     HIP_TRY(hipMemcpy(e->d_tw[v], tws[v].data(), sizeof(float2) * tws[v].size(), hipMemcpyHostToDevice));
   }
+  const std::vector<double2> lut = lut64_table();
+  HIP_TRY(hipMalloc(&e->d_lut64, sizeof(double2) * lut.size()));
+  HIP_TRY(hipMemcpy(e->d_lut64, lut.data(), sizeof(double2) * lut.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&e->d_tw64, sizeof(double2) * tw64.size()));
   HIP_TRY(hipMemcpy(e->d_tw64, tw64.data(), sizeof(double2) * tw64.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&e->d_f_rel64, sizeof(double) * S));
@@ -400,6 +431,7 @@ int32_t mimo_engine_run(mimo_engine* e, uint64_t seed, uint64_t first_trial, uin
   }
   p.f_over_c = e->d_f_over_c;
   p.tx_pos = e->d_tx_pos;
+  p.lut = e->d_lut64;
   p.n_ant = c.n_ant;
   p.n_sc = c.n_sub_carr;
   const int L = (int)std::lround(std::sqrt((double)c.constel_size));
@@ -495,6 +527,7 @@ void mimo_engine_destroy(mimo_engine* e) {
     (void)hipFree(e->d_tw[1]);
     (void)hipFree(e->d_f_rel);
     (void)hipFree(e->d_tw64);
+    (void)hipFree(e->d_lut64);
     (void)hipFree(e->d_f_rel64);
     (void)hipFree(e->d_ant_rel64);
     (void)hipFree(e->d_f_over_c);

@@ -57,7 +57,7 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, Key key) {
 //
 // fp32: v_sin/v_cos take revolutions, so 2*pi*u2 is never formed; v_log is log2, and the
 // scale argument c = -ln(2) scale^2 returns scale * CN(0,1) at no extra cost.
-// fp64: full-precision software ln / sincos (real.h); c = -scale^2 (natural log).
+// fp64: LDS-table ln / sincos and a Newton sqrt (real.h, ~1.5 ulp); c = -scale^2 (natural log).
 // bm_c<R>(scale^2) builds c for either.
 constexpr float kNegLn2 = -0.69314718055994531f;
 template <typename R>
@@ -74,8 +74,9 @@ __device__ __forceinline__ double bm_c<double>(double scale2) {
 __device__ __forceinline__ float bm_log(uint32_t w0, float) {
   return __builtin_amdgcn_logf(fmaf((float)w0, 2.3283064365386963e-10f, 1.1641532182693481e-10f));
 }
+// fp64: LDS-table ln (real.h ln_lut; the trial kernel loads lut64 first).
 __device__ __forceinline__ double bm_log(uint32_t w0, double) {
-  return ln_pos(((double)w0 + 0.5) * 2.3283064365386963e-10);  // exact argument
+  return ln_lut(((double)w0 + 0.5) * 2.3283064365386963e-10);  // exact argument
 }
 
 __device__ __forceinline__ float2 box_muller(uint32_t w0, uint32_t w1, float c = kNegLn2) {
@@ -88,9 +89,9 @@ __device__ __forceinline__ float2 box_muller(uint32_t w0, uint32_t w1, float c =
   return make_float2(rho * __builtin_amdgcn_cosf(u2), rho * __builtin_amdgcn_sinf(u2));
 }
 __device__ __forceinline__ double2 box_muller(uint32_t w0, uint32_t w1, double c) {
-  const double rho = __builtin_sqrt(c * bm_log(w0, 0.0));
+  const double rho = sqrt_nr(c * bm_log(w0, 0.0));  // argument > 0: u1 < 1 always
   double s, co;
-  sincos_rev((double)w1 * 2.3283064365386963e-10, s, co);  // exact revolutions
+  sincos_lut(w1, s, co);  // revolutions w1 2^-32, from the word itself
   return make_double2(rho * co, rho * s);
 }
 

@@ -232,9 +232,14 @@ struct TeamFft {
   // Padding of exchange S: one slot per 2^PSH elements.  Exchange 0 (stage 0 writes
   // 16t + r) uses 1/16 (MIMO_PAD0_SHIFT): it halves that exchange's modelled bank
   // conflicts (tools/lds_conflicts.py); later exchanges use 1/32.
-  static constexpr int psh(int S) { return S == 0 ? MIMO_PAD0_SHIFT : MIMO_PADN_SHIFT; }
-  static constexpr int LDS_ELEMS =
-      F + F / (1 << (MIMO_PAD0_SHIFT < MIMO_PADN_SHIFT ? MIMO_PAD0_SHIFT : MIMO_PADN_SHIFT));
+  // fp64 elements are 16 B (ds_write_b128: 8-lane groups over 32 banks), where stage 0's
+  // stride-R writes need one pad slot per 8 elements: the modelled extra LDS cycles of
+  // exchange 0 drop 3x (tools/lds_conflicts.py; the model reproduces SQ_LDS_BANK_CONFLICT
+  // of the 1/16 layout exactly, profiles/r02/abl64).  F = 8192 keeps 1/16: its 16 KiB
+  // more would not fit the 160 KiB LDS next to the fp64 tables and the CSI scratch.
+  static constexpr int PAD0 = (sizeof(Re) == 8 && F < 8192) ? 3 : MIMO_PAD0_SHIFT;
+  static constexpr int psh(int S) { return S == 0 ? PAD0 : MIMO_PADN_SHIFT; }
+  static constexpr int LDS_ELEMS = F + F / (1 << (PAD0 < MIMO_PADN_SHIFT ? PAD0 : MIMO_PADN_SHIFT));
   static_assert((1 << LOG_F) == F && (1 << LOG_P) == P && P >= 2, "power-of-two sizes");
 
   static constexpr int bits(int s) { return fft_bits(F, P, s); }
@@ -345,6 +350,8 @@ struct TeamFft {
   // Measured -1.1 % (F 2048), -1.5 % (F 4096), +0.9 % (F 8192: more stages held live).
   // fp64: off (the prefetched twiddles would hold ~32 more VGPRs across a transform).
   static constexpr bool PREFETCH = MIMO_TW_PREFETCH && F <= 4096 && sizeof(Re) == 4;
+  // Base holds w(2^k) for k < kMaxB; a stage reads k < bits(S) <= LOG_P.
+  static_assert(!PREFETCH || LOG_P <= kMaxB, "Base too small for the plan's largest radix");
   struct Base {
     C v[NST][kMaxB];
   };

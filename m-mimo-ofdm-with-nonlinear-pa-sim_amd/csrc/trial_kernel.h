@@ -66,6 +66,7 @@ struct TrialParams {
   const R* f_rel;                // [S]  fc / f_k      (f_k float32-quantised as in the reference)
   const double* f_over_c;        // [S]  f_k / c       (LoS / two-path phases)
   const double* tx_pos;          // [A*3]
+  const double2* lut;            // [kLut64] fp64 ln / sincos tables (real.h; fp64 instances only)
   int n_ant, n_sc, qam_l, half_bits;
   uint32_t label_mask;
   int pa_kind, cnc_pa_kind;
@@ -529,6 +530,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   const Key key{(uint32_t)p.seed, (uint32_t)(p.seed >> 32)};
   const int S = p.n_sc, A = p.n_ant, L = p.qam_l, hb = p.half_bits;
   const R inv_sqrt_f = p.inv_sqrt_f;
+  if constexpr (sizeof(R) == 8) {  // Box-Muller tables (real.h ln_lut / sincos_lut) into LDS
+    for (int i = t; i < kLut64; i += T) lut64[i] = p.lut[i];
+    __syncthreads();
+  }
 
   // RX position for LoS / two-path (mp_model.py:190-201; y uses rx_loc_x, a reference quirk)
   double rx[3] = {0.0, 0.0, 0.0};

@@ -26,9 +26,10 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 16)
     ap.add_argument("--iters", default="0")
     ap.add_argument("--workload", default="2")
+    ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     args = ap.parse_args()
     variants = [dict(kv.split("=", 1) for kv in v.split(",") if kv) for v in (args.var or [""])]
-    eng = bench.make_engine(0, args.workload)
+    eng = bench.make_engine(0, args.workload, args.precision)
     iters = [int(x) for x in args.iters.split(",")]
     res = {i: [] for i in range(len(variants))}
     errs = {}

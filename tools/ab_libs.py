@@ -27,13 +27,14 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 16)
     ap.add_argument("--iters", default="0")
     ap.add_argument("--workload", default="2")
+    ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     args = ap.parse_args()
     iters = [int(x) for x in args.iters.split(",")]
     handles, engines = [], []
     for path in args.libs:
         _engine._lib, _engine.LIB_PATH = None, os.path.abspath(path)
         handles.append(_engine.lib())
-        engines.append(bench.make_engine(0, args.workload))
+        engines.append(bench.make_engine(0, args.workload, args.precision))
     res = {i: [] for i in range(len(engines))}
     errs = {}
     for r in range(args.rounds + 1):

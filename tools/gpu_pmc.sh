@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc}
 mkdir -p $OUT
-BENCH="bench.py --no-cpu-baseline --steps 2 --warmup 1"
+BENCH="bench.py --no-cpu-baseline --steps 2 --warmup 1 ${PMC_BENCH_ARGS:-}"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" \
