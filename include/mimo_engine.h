@@ -9,6 +9,8 @@
  *     mimo_engine_create        <- Link.__init__                       mp_model.py:32-87
  *     mimo_engine_set_point     <- Link.update_distortion / set_snr    mp_model.py:230-251
  *     mimo_engine_run           <- Link.simulate (trial loop)          mp_model.py:89-228
+ *     mimo_engine_run_points    <- the drivers' grid loops over (IBO, Eb/N0), one launch
+ *                                  for many points   main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:100-215
  *   fine seams (float64 stage kernels, caller-owned host arrays)
  *     mimo_qam_map              <- modulation.modulate                 modulation.py:13-25
  *     mimo_qam_slice            <- demodulate / symbol_detection       modulation.py:63-88,138-146
@@ -37,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MIMO_ABI_VERSION 2
+#define MIMO_ABI_VERSION 3
 
 enum { MIMO_OK = 0, MIMO_EINVAL = -1, MIMO_EHIP = -2, MIMO_ENOKERNEL = -3, MIMO_ENOMEM = -4 };
 enum { MIMO_PA_NONE = 0, MIMO_PA_SOFTLIM = 1, MIMO_PA_RAPP = 2, MIMO_PA_TOI = 3 };
@@ -97,6 +99,18 @@ int32_t mimo_engine_set_point(mimo_engine* e, const mimo_point* pt);
 int32_t mimo_engine_run(mimo_engine* e, uint64_t seed, uint64_t first_trial, uint64_t n_trials,
                         const int32_t* iters, int32_t n_iters, int32_t incl_clean,
                         uint64_t* err_out, uint64_t* bits_out, uint32_t* per_trial);
+/* Many grid points of the same system in one go (BASELINE config 4 sweeps): point i runs
+ * trials [first_trial[i], first_trial[i] + n_trials[i]) keyed by seeds[i] with the
+ * parameters points[i].  Every point's trials are a contiguous block range of one kernel
+ * launch (launches hold up to 2^20 trials), so a grid of small points fills the GPU.
+ * All points share iters / incl_clean and must agree on CSI error on / off.
+ * err_out / bits_out: [n_points][n_idx] totals (ADDED to).  per_trial: optional
+ * [sum n_trials][n_idx] counts in point order, NULL to skip.  mimo_engine_run(...) is
+ * this call with the engine's current point. */
+int32_t mimo_engine_run_points(mimo_engine* e, int32_t n_points, const mimo_point* points, const uint64_t* seeds,
+                               const uint64_t* first_trial, const uint64_t* n_trials, const int32_t* iters,
+                               int32_t n_iters, int32_t incl_clean, uint64_t* err_out, uint64_t* bits_out,
+                               uint32_t* per_trial);
 /* Device time of the trial kernels of the last run, in ms (HIP events on the engine stream). */
 double mimo_engine_last_kernel_ms(const mimo_engine* e);
 /* Which kernel instance the current config selects: "F=2048 T=128 slots=8 aligned ..." */

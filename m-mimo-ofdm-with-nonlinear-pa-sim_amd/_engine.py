@@ -58,6 +58,9 @@ SYMBOLS = {
     "mimo_engine_set_point": (ctypes.c_int32, [ctypes.c_void_p, ctypes.POINTER(MimoPoint)]),
     "mimo_engine_run": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _i32p,
                                          ctypes.c_int32, ctypes.c_int32, _u64p, _u64p, _u32p]),
+    "mimo_engine_run_points": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(MimoPoint), _u64p,
+                                                _u64p, _u64p, _i32p, ctypes.c_int32, ctypes.c_int32, _u64p, _u64p,
+                                                _u32p]),
     "mimo_engine_last_kernel_ms": (ctypes.c_double, [ctypes.c_void_p]),
     "mimo_engine_describe": (ctypes.c_char_p, [ctypes.c_void_p]),
     "mimo_engine_destroy": (None, [ctypes.c_void_p]),
@@ -144,14 +147,44 @@ class Engine:
         self._h, self._L = h, L   # the library this handle belongs to
         self.n_sub_carr, self.constel_size = n_sub_carr, constel_size
 
-    def set_point(self, ibo_db, snr_db, avg_symbol_power, pa_kind, sat_pow=0.0, p_hardness=0.0, toi_coeff=0.0,
-                  cnc_pa_kind=None, cnc_sat_pow=0.0, cnc_toi_coeff=0.0, cnc_alpha=1.0, csi_eps=None):
-        pt = MimoPoint(ibo_db=float(ibo_db), snr_db=float(snr_db), avg_symbol_power=float(avg_symbol_power),
-                       pa_kind=PA_KINDS[pa_kind], cnc_pa_kind=PA_KINDS[cnc_pa_kind or pa_kind],
-                       sat_pow=float(sat_pow), p_hardness=float(p_hardness), toi_coeff=float(toi_coeff),
-                       cnc_sat_pow=float(cnc_sat_pow), cnc_toi_coeff=float(cnc_toi_coeff),
-                       cnc_alpha=float(cnc_alpha), csi_eps=-1.0 if csi_eps is None else float(csi_eps))
+    @staticmethod
+    def make_point(ibo_db, snr_db, avg_symbol_power, pa_kind, sat_pow=0.0, p_hardness=0.0, toi_coeff=0.0,
+                   cnc_pa_kind=None, cnc_sat_pow=0.0, cnc_toi_coeff=0.0, cnc_alpha=1.0, csi_eps=None):
+        """A mimo_point from the per-point object state (Link.point_params() keys)."""
+        return MimoPoint(ibo_db=float(ibo_db), snr_db=float(snr_db), avg_symbol_power=float(avg_symbol_power),
+                         pa_kind=PA_KINDS[pa_kind], cnc_pa_kind=PA_KINDS[cnc_pa_kind or pa_kind],
+                         sat_pow=float(sat_pow), p_hardness=float(p_hardness), toi_coeff=float(toi_coeff),
+                         cnc_sat_pow=float(cnc_sat_pow), cnc_toi_coeff=float(cnc_toi_coeff),
+                         cnc_alpha=float(cnc_alpha), csi_eps=-1.0 if csi_eps is None else float(csi_eps))
+
+    def set_point(self, ibo_db, snr_db, avg_symbol_power, pa_kind, **kw):
+        pt = self.make_point(ibo_db, snr_db, avg_symbol_power, pa_kind, **kw)
         _check(self._L.mimo_engine_set_point(self._h, ctypes.byref(pt)))
+
+    def run_points(self, points, seeds, first_trials, n_trials, iters, incl_clean=False, per_trial=False):
+        """Many grid points in as few launches as possible (mimo_engine_run_points).
+        points: list of dicts (make_point keywords) or MimoPoint.  -> (err[P, n_idx],
+        bits[P, n_idx], per_trial[sum n_trials, n_idx] or None)."""
+        P = len(points)
+        arr = (MimoPoint * max(1, P))()
+        for i, pt in enumerate(points):
+            arr[i] = pt if isinstance(pt, MimoPoint) else self.make_point(**pt)
+        it = _c(sorted(set(int(i) for i in iters)), np.int32)
+        n_idx = len(it) + (1 if incl_clean else 0)
+        sd = _c(np.asarray([int(x) & 0xFFFFFFFFFFFFFFFF for x in seeds], dtype=np.uint64).reshape(-1), np.uint64)
+        ft = _c(np.asarray(first_trials, dtype=np.uint64).reshape(-1), np.uint64)
+        nt = _c(np.asarray(n_trials, dtype=np.uint64).reshape(-1), np.uint64)
+        if not (len(sd) == len(ft) == len(nt) == P):
+            raise ValueError("points, seeds, first_trials and n_trials must have the same length")
+        err = np.zeros((P, n_idx), np.uint64)
+        bits = np.zeros((P, n_idx), np.uint64)
+        pt = np.zeros((int(nt.sum()), n_idx), np.uint32) if per_trial else None
+        _check(self._L.mimo_engine_run_points(self._h, P, arr, _ptr(sd, ctypes.c_uint64), _ptr(ft, ctypes.c_uint64),
+                                              _ptr(nt, ctypes.c_uint64), _ptr(it, ctypes.c_int32), len(it),
+                                              int(bool(incl_clean)), _ptr(err, ctypes.c_uint64),
+                                              _ptr(bits, ctypes.c_uint64),
+                                              _ptr(pt, ctypes.c_uint32) if pt is not None else None))
+        return err, bits, pt
 
     def run(self, seed, first_trial, n_trials, iters, incl_clean=False, per_trial=False):
         """-> (err[n_idx], bits[n_idx], per_trial[n_trials, n_idx] or None)."""

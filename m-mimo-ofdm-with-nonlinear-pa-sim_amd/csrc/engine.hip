@@ -36,17 +36,17 @@ constexpr double kSpeedOfLight = 299792458.0;  // scipy.constants.c
 
 bool is_pow2(long v) { return v > 0 && (v & (v - 1)) == 0; }
 
-// Sum of per-trial counts over trials, per counter index (deterministic order-free
-// integer sums; one 64-bit atomic per wave).
-__global__ void reduce_counts(const uint32_t* __restrict__ c, uint64_t n_trials, int n_idx,
-                              unsigned long long* __restrict__ tot) {
-  const int idx = blockIdx.y;
+// Per-point sums of the per-trial counts of one launch: block (seg, idx) adds the counts of
+// blocks [start[seg], start[seg + 1]) into tot[point_of[seg]][idx] (integer sums: the
+// order does not matter; one 64-bit atomic per wave).
+__global__ void reduce_counts(const uint32_t* __restrict__ c, const uint32_t* __restrict__ start,
+                              const int32_t* __restrict__ point_of, int n_idx, unsigned long long* __restrict__ tot) {
+  const int seg = blockIdx.x, idx = blockIdx.y;
   unsigned long long acc = 0;
-  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_trials; t += (uint64_t)gridDim.x * blockDim.x)
-    acc += c[t * n_idx + idx];
+  for (uint32_t t = start[seg] + threadIdx.x; t < start[seg + 1]; t += blockDim.x) acc += c[(size_t)t * n_idx + idx];
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
-  if ((threadIdx.x & 63) == 0) atomicAdd(&tot[idx], acc);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&tot[(size_t)point_of[seg] * n_idx + idx], acc);
 }
 
 // Bussgang gain of modulation.py:178-189 as a function of gamma^2.
@@ -145,7 +145,13 @@ struct mimo_engine {
   double* d_tx_pos = nullptr;
   uint32_t* d_counts = nullptr;
   size_t counts_cap = 0;
-  unsigned long long* d_tot = nullptr;
+  unsigned long long* d_tot = nullptr;    // [points][n_idx] totals of one run
+  size_t tot_cap = 0;
+  void* d_points = nullptr;                // TrialParams<R>[segments of one launch]
+  size_t points_cap = 0;                   // bytes
+  uint32_t* d_start = nullptr;             // [segments + 1] block offsets
+  int32_t* d_point_of = nullptr;           // [segments] point index
+  size_t start_cap = 0, point_of_cap = 0;
   double d0 = 1.0;
   double last_ms = 0.0;
   std::string desc;
@@ -242,6 +248,55 @@ int validate_config(const mimo_config* c) {
   return MIMO_OK;
 }
 
+int validate_point(const mimo_engine* e, const mimo_point* pt) {
+  auto bad_kind = [](int k) { return k < MIMO_PA_NONE || k > MIMO_PA_TOI; };
+  if (bad_kind(pt->pa_kind) || bad_kind(pt->cnc_pa_kind)) return fail(MIMO_EINVAL, "unknown PA kind");
+  if ((pt->pa_kind == MIMO_PA_SOFTLIM || pt->pa_kind == MIMO_PA_RAPP) && !(pt->sat_pow > 0))
+    return fail(MIMO_EINVAL, "sat_pow must be > 0");
+  if (pt->pa_kind == MIMO_PA_RAPP && !(pt->p_hardness > 0)) return fail(MIMO_EINVAL, "p_hardness must be > 0");
+  if (!(pt->cnc_alpha != 0)) return fail(MIMO_EINVAL, "cnc_alpha must be non-zero");
+  if (pt->csi_eps >= 1.0) return fail(MIMO_EINVAL, "csi_eps must be < 1");
+  if (pt->csi_eps >= 0 && e->cfg.n_ant > mimo::kMaxCsiAnt) return fail(MIMO_EINVAL, "CSI error supports n_ant <= 512");
+  return MIMO_OK;
+}
+
+// Per-point fields of the kernel parameters (the reference's per-point object state).
+template <typename R>
+void fill_point(const mimo_engine* e, const mimo_point& pt, uint64_t seed, uint64_t first_trial,
+                mimo::TrialParams<R>& p) {
+  const mimo_config& c = e->cfg;
+  const bool csi = pt.csi_eps >= 0;
+  p.seed = seed;
+  p.first_trial = first_trial;
+  p.pa_kind = pt.pa_kind;
+  p.cnc_pa_kind = pt.cnc_pa_kind;
+  p.sat_tx = (R)pt.sat_pow;
+  p.sqrt_sat_tx = (R)std::sqrt(std::max(pt.sat_pow, 0.0));
+  p.inv_sat_tx = pt.sat_pow > 0 ? (R)(1.0 / pt.sat_pow) : R(0);
+  p.rapp_p = (R)pt.p_hardness;
+  p.toi_tx = (R)pt.toi_coeff;
+  p.sat_cnc = (R)pt.cnc_sat_pow;
+  p.sqrt_sat_cnc = (R)std::sqrt(std::max(pt.cnc_sat_pow, 0.0));
+  p.inv_sat_cnc = pt.cnc_sat_pow > 0 ? (R)(1.0 / pt.cnc_sat_pow) : R(0);
+  p.toi_cnc = (R)pt.cnc_toi_coeff;
+  p.inv_alpha_cnc = (R)(1.0 / pt.cnc_alpha);
+  p.alpha_c = (R)(std::pow(10.0, pt.ibo_db / 10.0) * c.n_sub_carr / c.n_ant);
+  fit_alpha(std::pow(10.0, pt.ibo_db / 10.0), p);
+  p.es_over_snr = (R)(pt.avg_symbol_power / std::pow(10.0, pt.snr_db / 10.0));
+  p.csi_a = csi ? (R)std::sqrt(1.0 - pt.csi_eps * pt.csi_eps) : R(1);
+  p.csi_b = csi ? (R)pt.csi_eps : R(0);
+}
+
+template <typename T>
+int ensure_cap(T*& ptr, size_t& cap, size_t need) {
+  if (need <= cap) return MIMO_OK;
+  if (ptr) HIP_TRY(hipFree(ptr));
+  ptr = nullptr;
+  HIP_TRY(hipMalloc(&ptr, need * sizeof(T)));
+  cap = need;
+  return MIMO_OK;
+}
+
 int ensure_device(mimo_engine* e) {
   if (e->ready) return MIMO_OK;
   if (e->cfg.device >= 0) HIP_TRY(hipSetDevice(e->cfg.device));
@@ -317,7 +372,6 @@ int ensure_device(mimo_engine* e) {
   HIP_TRY(hipMalloc(&e->d_f_over_c, sizeof(double) * S));
   HIP_TRY(hipMalloc(&e->d_ant_rel, sizeof(float) * A));
   HIP_TRY(hipMalloc(&e->d_tx_pos, sizeof(double) * 3 * A));
-  HIP_TRY(hipMalloc(&e->d_tot, sizeof(unsigned long long) * 64));
   HIP_TRY(hipMemcpy(e->d_f_rel, f_rel.data(), sizeof(float) * S, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_f_over_c, f_over_c.data(), sizeof(double) * S, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_ant_rel, ant_rel.data(), sizeof(float) * A, hipMemcpyHostToDevice));
@@ -360,23 +414,23 @@ mimo_engine* mimo_engine_create(const mimo_config* cfg) {
 
 int32_t mimo_engine_set_point(mimo_engine* e, const mimo_point* pt) {
   if (!e || !pt) return fail(MIMO_EINVAL, "null argument");
-  auto bad_kind = [](int k) { return k < MIMO_PA_NONE || k > MIMO_PA_TOI; };
-  if (bad_kind(pt->pa_kind) || bad_kind(pt->cnc_pa_kind)) return fail(MIMO_EINVAL, "unknown PA kind");
-  if ((pt->pa_kind == MIMO_PA_SOFTLIM || pt->pa_kind == MIMO_PA_RAPP) && !(pt->sat_pow > 0))
-    return fail(MIMO_EINVAL, "sat_pow must be > 0");
-  if (pt->pa_kind == MIMO_PA_RAPP && !(pt->p_hardness > 0)) return fail(MIMO_EINVAL, "p_hardness must be > 0");
-  if (!(pt->cnc_alpha != 0)) return fail(MIMO_EINVAL, "cnc_alpha must be non-zero");
-  if (pt->csi_eps >= 1.0) return fail(MIMO_EINVAL, "csi_eps must be < 1");
-  if (pt->csi_eps >= 0 && e->cfg.n_ant > mimo::kMaxCsiAnt) return fail(MIMO_EINVAL, "CSI error supports n_ant <= 512");
+  if (int rc = validate_point(e, pt)) return rc;
   e->pt = *pt;
   e->have_point = true;
   return MIMO_OK;
 }
 
-int32_t mimo_engine_run(mimo_engine* e, uint64_t seed, uint64_t first_trial, uint64_t n_trials, const int32_t* iters,
-                        int32_t n_iters, int32_t incl_clean, uint64_t* err_out, uint64_t* bits_out, uint32_t* per_trial) {
-  if (!e) return fail(MIMO_EINVAL, "null engine");
-  if (!e->have_point) return fail(MIMO_EINVAL, "mimo_engine_set_point was not called");
+}  // extern "C"
+
+namespace {
+
+// Runs n_points grid points of one system in as few launches as possible: every point's
+// trials become a contiguous range of blocks of one launch (split across launches only
+// beyond kChunk blocks), and a segmented reduction sums each point's counts.
+int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64_t* seeds,
+               const uint64_t* first_trial, const uint64_t* n_trials, const int32_t* iters, int32_t n_iters,
+               int32_t incl_clean, uint64_t* err_out, uint64_t* bits_out, uint32_t* per_trial) {
+  if (n_points < 0) return fail(MIMO_EINVAL, "n_points must be >= 0");
   if (n_iters < 1 || !iters) return fail(MIMO_EINVAL, "at least one iteration index is required");
   uint32_t rec_mask = 0;
   int max_iter = -1;
@@ -387,14 +441,19 @@ int32_t mimo_engine_run(mimo_engine* e, uint64_t seed, uint64_t first_trial, uin
     max_iter = std::max(max_iter, (int)iters[i]);
   }
   if (!err_out || !bits_out) return fail(MIMO_EINVAL, "null counters");
+  if (n_points == 0) return MIMO_OK;
+  if (!pts || !seeds || !first_trial || !n_trials) return fail(MIMO_EINVAL, "null point arrays");
   const int n_idx = n_iters + (incl_clean ? 1 : 0);
   const mimo_config& c = e->cfg;
-  const mimo_point& pt = e->pt;
-  if (n_trials + first_trial > (1ull << 32)) return fail(MIMO_EINVAL, "trial index must fit 32 bits");
-  const bool csi = pt.csi_eps >= 0;
+  const bool csi = pts[0].csi_eps >= 0;
+  for (int i = 0; i < n_points; ++i) {
+    if (int rc = validate_point(e, &pts[i])) return rc;
+    if ((pts[i].csi_eps >= 0) != csi) return fail(MIMO_EINVAL, "all points of one run must agree on CSI error on/off");
+    if (n_trials[i] + first_trial[i] > (1ull << 32) || first_trial[i] >= (1ull << 32))
+      return fail(MIMO_EINVAL, "trial index must fit 32 bits");
+  }
   const mimo::InstanceKey key = select_instance(e, csi);
   if (int rc = ensure_device(e)) return rc;
-
   if (!c.reroll_chan && c.channel_kind != MIMO_CH_RAYLEIGH) {
     // fixed RX: jitter span 0 around (x0, x0); only consistent when rx_y == rx_x
     if (c.rx_pos[1] != c.rx_pos[0]) return fail(MIMO_EINVAL, "reroll_chan=0 requires rx_pos[1] == rx_pos[0]");
@@ -404,105 +463,167 @@ int32_t mimo_engine_run(mimo_engine* e, uint64_t seed, uint64_t first_trial, uin
            key.aligned ? "aligned" : "generic", key.ch, (int)key.csi, key.f64 ? "f64" : "f32");
   e->desc = buf;
 
-  const uint64_t chunk_max = 1ull << 20;
-  const size_t need = (size_t)std::min<uint64_t>(n_trials, chunk_max) * n_idx;
-  if (need > e->counts_cap) {
-    if (e->d_counts) HIP_TRY(hipFree(e->d_counts));
-    HIP_TRY(hipMalloc(&e->d_counts, need * sizeof(uint32_t)));
-    e->counts_cap = need;
+  // segments (point, first trial, count) packed into launches of <= kChunk blocks
+  constexpr uint64_t kChunk = 1ull << 20;
+  struct Seg {
+    int point;
+    uint64_t first, n;
+  };
+  std::vector<std::vector<Seg>> launches(1);
+  uint64_t fill = 0;
+  for (int i = 0; i < n_points; ++i) {
+    uint64_t done = 0;
+    while (done < n_trials[i]) {
+      if (fill == kChunk) {
+        launches.emplace_back();
+        fill = 0;
+      }
+      const uint64_t n = std::min(n_trials[i] - done, kChunk - fill);
+      launches.back().push_back(Seg{i, first_trial[i] + done, n});
+      done += n;
+      fill += n;
+    }
   }
-  HIP_TRY(hipMemsetAsync(e->d_tot, 0, sizeof(unsigned long long) * n_idx, e->stream));
+  size_t max_seg = 0;
+  for (auto& l : launches) max_seg = std::max(max_seg, l.size());
+  if (int rc = ensure_cap(e->d_counts, e->counts_cap, (size_t)kChunk * n_idx)) return rc;
+  if (int rc = ensure_cap(e->d_tot, e->tot_cap, (size_t)n_points * n_idx)) return rc;
+  if (int rc = ensure_cap(e->d_start, e->start_cap, max_seg + 1)) return rc;
+  if (int rc = ensure_cap(e->d_point_of, e->point_of_cap, max_seg)) return rc;
+  HIP_TRY(hipMemsetAsync(e->d_tot, 0, sizeof(unsigned long long) * n_points * n_idx, e->stream));
   double ms_total = 0.0;
+  uint64_t rows_done = 0;
 
-  // Kernel parameters in the instance's arithmetic type, then the batch launches.
   auto run_as = [&](auto zero) -> int {
-  using R = decltype(zero);
-  constexpr bool F64 = sizeof(R) == 8;
-  mimo::TrialParams<R> p{};
-  p.seed = seed;
-  if constexpr (F64) {
-    p.tw = e->d_tw64;
-    p.ant_rel = e->d_ant_rel64;
-    p.f_rel = e->d_f_rel64;
-  } else {
-    p.tw = e->d_tw[key.T == mimo::team_size(c.n_fft) ? 0 : 1];
-    p.ant_rel = e->d_ant_rel;
-    p.f_rel = e->d_f_rel;
-  }
-  p.f_over_c = e->d_f_over_c;
-  p.tx_pos = e->d_tx_pos;
-  p.lut = e->d_lut64;
-  p.n_ant = c.n_ant;
-  p.n_sc = c.n_sub_carr;
-  const int L = (int)std::lround(std::sqrt((double)c.constel_size));
-  p.qam_l = L;
-  p.half_bits = (int)std::lround(std::log2((double)L));
-  p.label_mask = (uint32_t)c.constel_size - 1u;
-  p.pa_kind = pt.pa_kind;
-  p.cnc_pa_kind = pt.cnc_pa_kind;
-  p.sat_tx = (R)pt.sat_pow;
-  p.sqrt_sat_tx = (R)std::sqrt(std::max(pt.sat_pow, 0.0));
-  p.inv_sat_tx = pt.sat_pow > 0 ? (R)(1.0 / pt.sat_pow) : R(0);
-  p.rapp_p = (R)pt.p_hardness;
-  p.toi_tx = (R)pt.toi_coeff;
-  p.sat_cnc = (R)pt.cnc_sat_pow;
-  p.sqrt_sat_cnc = (R)std::sqrt(std::max(pt.cnc_sat_pow, 0.0));
-  p.inv_sat_cnc = pt.cnc_sat_pow > 0 ? (R)(1.0 / pt.cnc_sat_pow) : R(0);
-  p.toi_cnc = (R)pt.cnc_toi_coeff;
-  p.inv_alpha_cnc = (R)(1.0 / pt.cnc_alpha);
-  p.alpha_c = (R)(std::pow(10.0, pt.ibo_db / 10.0) * c.n_sub_carr / c.n_ant);
-  fit_alpha(std::pow(10.0, pt.ibo_db / 10.0), p);
-  p.inv_vk0 = (R)((double)c.n_ant / c.n_sub_carr);
-  p.es_over_snr = (R)(pt.avg_symbol_power / std::pow(10.0, pt.snr_db / 10.0));
-  p.csi_a = csi ? (R)std::sqrt(1.0 - pt.csi_eps * pt.csi_eps) : R(1);
-  p.csi_b = csi ? (R)pt.csi_eps : R(0);
-  p.inv_sqrt_f = (R)(1.0 / std::sqrt((double)c.n_fft));
-  p.receiver = c.receiver_kind;
-  p.max_iter = max_iter;
-  p.rec_mask = rec_mask;
-  p.incl_clean = incl_clean ? 1 : 0;
-  p.n_idx = n_idx;
-  p.rx_x0 = c.rx_pos[0];
-  p.rx_z = c.rx_pos[2];
-  p.rx_var = c.reroll_chan ? c.rx_loc_var : 0.0;
-  p.d0 = e->d0;
-  p.ablate = 0;
+    using R = decltype(zero);
+    using TP = mimo::TrialParams<R>;
+    constexpr bool F64 = sizeof(R) == 8;
+    TP base{};
+    if constexpr (F64) {
+      base.tw = e->d_tw64;
+      base.ant_rel = e->d_ant_rel64;
+      base.f_rel = e->d_f_rel64;
+    } else {
+      base.tw = e->d_tw[key.T == mimo::team_size(c.n_fft) ? 0 : 1];
+      base.ant_rel = e->d_ant_rel;
+      base.f_rel = e->d_f_rel;
+    }
+    base.f_over_c = e->d_f_over_c;
+    base.tx_pos = e->d_tx_pos;
+    base.lut = e->d_lut64;
+    base.n_ant = c.n_ant;
+    base.n_sc = c.n_sub_carr;
+    const int L = (int)std::lround(std::sqrt((double)c.constel_size));
+    base.qam_l = L;
+    base.half_bits = (int)std::lround(std::log2((double)L));
+    base.label_mask = (uint32_t)c.constel_size - 1u;
+    base.inv_vk0 = (R)((double)c.n_ant / c.n_sub_carr);
+    base.inv_sqrt_f = (R)(1.0 / std::sqrt((double)c.n_fft));
+    base.receiver = c.receiver_kind;
+    base.max_iter = max_iter;
+    base.rec_mask = rec_mask;
+    base.incl_clean = incl_clean ? 1 : 0;
+    base.n_idx = n_idx;
+    base.rx_x0 = c.rx_pos[0];
+    base.rx_z = c.rx_pos[2];
+    base.rx_var = c.reroll_chan ? c.rx_loc_var : 0.0;
+    base.d0 = e->d0;
+    base.ablate = 0;
 #ifdef MIMO_ABLATION
-  if (const char* env = std::getenv("MIMO_ABLATE")) p.ablate = (uint32_t)std::strtoul(env, nullptr, 0);
+    if (const char* env = std::getenv("MIMO_ABLATE")) base.ablate = (uint32_t)std::strtoul(env, nullptr, 0);
 #endif
-  for (uint64_t done = 0; done < n_trials; done += chunk_max) {
-    const uint64_t nt = std::min<uint64_t>(chunk_max, n_trials - done);
-    p.first_trial = first_trial + done;
-    p.counts = e->d_counts;
-    HIP_TRY(hipEventRecord(e->ev0, e->stream));
-    bool found = false;
-    hipError_t le = launch(key, dim3((unsigned)nt), e->stream, p, &found);
-    if (!found) return fail(MIMO_ENOKERNEL, std::string("no kernel instance for ") + buf);
-    if (le != hipSuccess) return fail(MIMO_EHIP, std::string("trial kernel launch: ") + hipGetErrorString(le));
-    HIP_TRY(hipEventRecord(e->ev1, e->stream));
-    hipLaunchKernelGGL(reduce_counts, dim3(64, n_idx), dim3(256), 0, e->stream, e->d_counts, nt, n_idx, e->d_tot);
-    HIP_TRY(hipGetLastError());
-    if (per_trial)
-      HIP_TRY(hipMemcpyAsync(per_trial + done * n_idx, e->d_counts, nt * n_idx * sizeof(uint32_t),
-                             hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipEventSynchronize(e->ev1));
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, e->ev0, e->ev1));
-    ms_total += ms;
-  }
-  return MIMO_OK;
+    base.counts = e->d_counts;
+    // per-point parameter table (host), built once
+    std::vector<TP> ptab(n_points, base);
+    for (int i = 0; i < n_points; ++i) fill_point(e, pts[i], seeds[i], 0, ptab[i]);
+    char* dp = static_cast<char*>(e->d_points);
+    if (int rc = ensure_cap(dp, e->points_cap, max_seg * sizeof(TP))) return rc;
+    e->d_points = dp;
+    std::vector<TP> seg_tab;
+    std::vector<uint32_t> start;
+    std::vector<int32_t> point_of;
+    for (auto& l : launches) {
+      seg_tab.clear();
+      start.assign(1, 0u);
+      point_of.clear();
+      for (auto& sg : l) {
+        TP q = ptab[sg.point];
+        q.first_trial = sg.first;
+        seg_tab.push_back(q);
+        start.push_back(start.back() + (uint32_t)sg.n);
+        point_of.push_back(sg.point);
+      }
+      const uint32_t nb = start.back();
+      TP kp = base;
+      kp.points = reinterpret_cast<const TP*>(e->d_points);
+      kp.point_start = e->d_start;
+      kp.n_points = (int)l.size();
+      kp.seed = seg_tab[0].seed;  // unused by the kernel (read from the table)
+      HIP_TRY(hipMemcpyAsync(e->d_points, seg_tab.data(), seg_tab.size() * sizeof(TP), hipMemcpyHostToDevice,
+                             e->stream));
+      HIP_TRY(hipMemcpyAsync(e->d_start, start.data(), start.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                             e->stream));
+      HIP_TRY(hipMemcpyAsync(e->d_point_of, point_of.data(), point_of.size() * sizeof(int32_t),
+                             hipMemcpyHostToDevice, e->stream));
+      HIP_TRY(hipEventRecord(e->ev0, e->stream));
+      bool found = false;
+      hipError_t le = launch(key, dim3(nb), e->stream, kp, &found);
+      if (!found) return fail(MIMO_ENOKERNEL, std::string("no kernel instance for ") + buf);
+      if (le != hipSuccess) return fail(MIMO_EHIP, std::string("trial kernel launch: ") + hipGetErrorString(le));
+      HIP_TRY(hipEventRecord(e->ev1, e->stream));
+      hipLaunchKernelGGL(reduce_counts, dim3((unsigned)l.size(), n_idx), dim3(256), 0, e->stream, e->d_counts,
+                         e->d_start, e->d_point_of, n_idx, e->d_tot);
+      HIP_TRY(hipGetLastError());
+      if (per_trial)
+        HIP_TRY(hipMemcpyAsync(per_trial + rows_done * n_idx, e->d_counts, (size_t)nb * n_idx * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, e->stream));
+      rows_done += nb;
+      // the host tables of the next launch are rewritten: wait for this one's copies
+      HIP_TRY(hipEventSynchronize(e->ev1));
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+      ms_total += ms;
+    }
+    return MIMO_OK;
   };
   if (int rc = key.f64 ? run_as(0.0) : run_as(0.0f)) return rc;
-  unsigned long long tot[64];
-  HIP_TRY(hipMemcpyAsync(tot, e->d_tot, sizeof(unsigned long long) * n_idx, hipMemcpyDeviceToHost, e->stream));
+  std::vector<unsigned long long> tot((size_t)n_points * n_idx);
+  HIP_TRY(hipMemcpyAsync(tot.data(), e->d_tot, sizeof(unsigned long long) * tot.size(), hipMemcpyDeviceToHost,
+                         e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   const uint64_t bits_per_trial = (uint64_t)c.n_sub_carr * (uint64_t)std::lround(std::log2((double)c.constel_size));
-  for (int i = 0; i < n_idx; ++i) {
-    err_out[i] += tot[i];
-    bits_out[i] += bits_per_trial * n_trials;
-  }
+  for (int i = 0; i < n_points; ++i)
+    for (int j = 0; j < n_idx; ++j) {
+      err_out[(size_t)i * n_idx + j] += tot[(size_t)i * n_idx + j];
+      bits_out[(size_t)i * n_idx + j] += bits_per_trial * n_trials[i];
+    }
   e->last_ms = ms_total;
   return MIMO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t mimo_engine_run(mimo_engine* e, uint64_t seed, uint64_t first_trial, uint64_t n_trials, const int32_t* iters,
+                        int32_t n_iters, int32_t incl_clean, uint64_t* err_out, uint64_t* bits_out, uint32_t* per_trial) {
+  if (!e) return fail(MIMO_EINVAL, "null engine");
+  if (!e->have_point) return fail(MIMO_EINVAL, "mimo_engine_set_point was not called");
+  if (n_trials == 0) {  // validate the iteration list, add nothing
+    return run_points(e, 0, nullptr, nullptr, nullptr, nullptr, iters, n_iters, incl_clean, err_out, bits_out,
+                      per_trial);
+  }
+  return run_points(e, 1, &e->pt, &seed, &first_trial, &n_trials, iters, n_iters, incl_clean, err_out, bits_out,
+                    per_trial);
+}
+
+int32_t mimo_engine_run_points(mimo_engine* e, int32_t n_points, const mimo_point* points, const uint64_t* seeds,
+                               const uint64_t* first_trial, const uint64_t* n_trials, const int32_t* iters,
+                               int32_t n_iters, int32_t incl_clean, uint64_t* err_out, uint64_t* bits_out,
+                               uint32_t* per_trial) {
+  if (!e) return fail(MIMO_EINVAL, "null engine");
+  return run_points(e, n_points, points, seeds, first_trial, n_trials, iters, n_iters, incl_clean, err_out, bits_out,
+                    per_trial);
 }
 
 double mimo_engine_last_kernel_ms(const mimo_engine* e) { return e ? e->last_ms : 0.0; }
@@ -533,8 +654,11 @@ void mimo_engine_destroy(mimo_engine* e) {
     (void)hipFree(e->d_f_over_c);
     (void)hipFree(e->d_ant_rel);
     (void)hipFree(e->d_tx_pos);
-    (void)hipFree(e->d_tot);
+    if (e->d_tot) (void)hipFree(e->d_tot);
     if (e->d_counts) (void)hipFree(e->d_counts);
+    if (e->d_points) (void)hipFree(e->d_points);
+    if (e->d_start) (void)hipFree(e->d_start);
+    if (e->d_point_of) (void)hipFree(e->d_point_of);
     (void)hipEventDestroy(e->ev0);
     (void)hipEventDestroy(e->ev1);
     (void)hipStreamDestroy(e->stream);

@@ -31,6 +31,9 @@
 #ifndef MIMO_TW_LOAD_MAX
 #define MIMO_TW_LOAD_MAX 64  // twiddle powers r <= this are loaded (1: square the rest; measured neutral)
 #endif
+#ifndef MIMO_TW_LOAD_ALL
+#define MIMO_TW_LOAD_ALL 0  // 1: load every twiddle power (no products; A/B knob)
+#endif
 #ifndef MIMO_TW_PREFETCH
 #define MIMO_TW_PREFETCH 1  // load every stage's base twiddles at the start of a transform (F <= 4096)
 #endif
@@ -349,7 +352,10 @@ struct TeamFft {
   static constexpr int kMaxB = 5;
   // Measured -1.1 % (F 2048), -1.5 % (F 4096), +0.9 % (F 8192: more stages held live).
   // fp64: off (the prefetched twiddles would hold ~32 more VGPRs across a transform).
-  static constexpr bool PREFETCH = MIMO_TW_PREFETCH && F <= 4096 && sizeof(Re) == 4;
+#ifndef MIMO_TW_PREFETCH64
+#define MIMO_TW_PREFETCH64 0
+#endif
+  static constexpr bool PREFETCH = MIMO_TW_PREFETCH && F <= 4096 && (sizeof(Re) == 4 || MIMO_TW_PREFETCH64);
   // Base holds w(2^k) for k < kMaxB; a stage reads k < bits(S) <= LOG_P.
   static_assert(!PREFETCH || LOG_P <= kMaxB, "Base too small for the plan's largest radix");
   struct Base {
@@ -404,7 +410,7 @@ struct TeamFft {
                   : MIMO_DIAG_NOTW == 1 ? mkc(Re(1), Re(0))  // diagnostic: no twiddle traffic
                   : MIMO_DIAG_NOTW == 2 ? opaque_tw(r)            // diagnostic: multiplies, no loads
                                         : gload(tws + r * NS, jm0);
-        } else if ((r & (r - 1)) == 0) {
+        } else if ((r & (r - 1)) == 0 || MIMO_TW_LOAD_ALL) {
           w0[r] = gload(tws + r * NS, jm0);
         } else {
           int hb = r;

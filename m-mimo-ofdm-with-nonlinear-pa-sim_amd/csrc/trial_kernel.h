@@ -87,6 +87,13 @@ struct TrialParams {
   int incl_clean, n_idx;
   double rx_x0, rx_z, rx_var, d0; // LoS / two-path geometry
   uint32_t ablate;               // diagnostic builds only (-DMIMO_ABLATION), see ABL_* below
+  // Multi-point launches (mimo_engine_run_points): the kernel argument carries the table;
+  // block b runs trial points[i].first_trial + b - point_start[i] of point i, where
+  // point_start[i] <= b < point_start[i + 1].  The per-point parameters (PA, AGC, noise,
+  // seed ...) are read from points[i] through the constant address space (scalar loads).
+  const TrialParams* points;     // [n_points] (device)
+  const uint32_t* point_start;   // [n_points + 1] block offsets (device)
+  int n_points;
 };
 
 // Ablation switches for cost breakdowns.  Compiled in only with -DMIMO_ABLATION
@@ -269,6 +276,9 @@ __device__ __forceinline__ void rapp_int(C (&d)[P], R inv_sat) {
 // PA on all P samples of a thread: one uniform branch on the kind, then a straight loop.
 template <int P, class C, typename R = real_of<C>>
 __device__ __forceinline__ void pa_block(int kind, C (&d)[P], R sat, R sqrt_sat, R inv_sat, R rapp_p, R toi) {
+#ifdef MIMO_DIAG_PA_SOFTLIM_ONLY  // ISA inspection only (tools/one_inst.hip): no other PA kinds
+  kind = PA_SOFTLIM;
+#endif
   if (kind == PA_SOFTLIM) {
 #pragma unroll
     for (int m = 0; m < P; ++m) d[m] = pa_apply(PA_SOFTLIM, d[m], sat, sqrt_sat, inv_sat, rapp_p, toi);
@@ -392,7 +402,8 @@ struct Channel {
 
   // |H|^2 of antenna a at the thread's slots (Rayleigh, FSPL factor f_rel left out as in
   // gen<false>): the same draws as gen(), magnitudes only.
-  static __device__ __forceinline__ void power(const Params& p, Key key, uint32_t trial, int a, int t,
+  template <class PP>
+  static __device__ __forceinline__ void power(const PP& p, Key key, uint32_t trial, int a, int t,
                                                R (&e2)[NSLOT]) {
     const int S = p.n_sc;
     const R sa = p.ant_rel[a];
@@ -435,8 +446,8 @@ struct Channel {
   // cancel in MRT, AGC and the SNR normalisation).  FREL = false leaves out the
   // per-sub-carrier FSPL factor fc/f_k, which the kernel then applies once per trial
   // (it cancels in the MRT precoder; see the kernel's AWGN step).
-  template <bool FREL>
-  static __device__ __forceinline__ void gen(const Params& p, Key key, uint32_t trial, int a, int t,
+  template <bool FREL, class PP>
+  static __device__ __forceinline__ void gen(const PP& p, Key key, uint32_t trial, int a, int t,
                                              const double (&rx)[3], C (&h)[NSLOT]) {
     const int S = p.n_sc;
     if constexpr (CH == CH_RAYLEIGH) {
@@ -503,8 +514,20 @@ struct Channel {
 // the LDS), SYMW_LDS = keep the pre-weighted symbols in LDS (thread-private) instead of
 // registers.  F = 2048 runs (3, 1, true): 25 KiB LDS and <= 168 VGPRs per 128-thread team.
 template <typename R, int F, int T, int NSLOT, bool ALIGNED, int CH, bool CSI, int MINW, int NBUF, bool SYMW_LDS>
-__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void trial_kernel(TrialParams<R> p) {
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void trial_kernel(TrialParams<R> p0) {
   using C = cx<R>;
+  // ---- which point and trial this block runs (uniform binary search over point_start)
+  uint32_t pi = 0;
+  if (p0.n_points > 1) {
+    uint32_t lo = 0, hi = (uint32_t)p0.n_points;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (p0.point_start[mid] <= blockIdx.x) lo = mid; else hi = mid;
+    }
+    pi = lo;
+  }
+  using CParams = const __attribute__((address_space(4))) TrialParams<R>;
+  CParams& p = *(CParams*)(p0.points + pi);
   using FFT = TeamFft<F, T, NBUF, R>;
   using SL = Slots<F, T, NSLOT, ALIGNED>;
   using CHN = Channel<R, F, T, NSLOT, ALIGNED, CH>;
@@ -526,7 +549,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   const int t = threadIdx.x;
   const bool t0 = (t == 0);
   const int lane = t & 63, wid = t >> 6;
-  const uint32_t trial = (uint32_t)(p.first_trial + blockIdx.x);
+  const uint32_t trial = (uint32_t)(p.first_trial + (blockIdx.x - p0.point_start[pi]));
   const Key key{(uint32_t)p.seed, (uint32_t)(p.seed >> 32)};
   const int S = p.n_sc, A = p.n_ant, L = p.qam_l, hb = p.half_bits;
   const R inv_sqrt_f = p.inv_sqrt_f;
@@ -780,7 +803,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     eta_p = ((valid_mask >> s) & 1u) ? fmar(gs, gs, eta_p) : eta_p;
   }
   const R eta = team_sum<T>(eta_p, red) / (R)S;
-  uint32_t* out = p.counts + (size_t)blockIdx.x * p.n_idx;
+  uint32_t* out = p0.counts + (size_t)blockIdx.x * p0.n_idx;
 
   auto record = [&](int idx, uint32_t errs) __attribute__((always_inline)) {
     const R tot = team_sum<T>((R)errs, red);

@@ -14,8 +14,14 @@ Differences, by design:
   channels (the reference replays one Rayleigh sequence in all processes, channel.py:209-212);
 * a clean-run trial reuses its distorted trial's draws (no PA: the IFFT->FFT round
   trip is the identity in-band), so both counters see the same channels and noise;
-* batches overshoot ``bits_sent_max`` by at most one batch, sized so they do not
-  (the reference overshoots by up to num_cores symbols).
+* trials run in batches (one kernel launch each) sized by ``next_batch``: a pilot
+  batch, then the number of trials the open counters still need to reach
+  ``n_err_min`` at their observed error rate (+5 %), never past ``bits_sent_max``;
+  the reference checks after every symbol and overshoots by up to num_cores symbols.
+
+``simulate_points`` runs the same trial loop for many grid points at once (one launch
+per round over every open point, ``mimo_engine_run_points``): bit-identical to calling
+``simulate`` point by point with the same seeds.
 """
 from __future__ import annotations
 
@@ -34,6 +40,30 @@ from modulation import OfdmQamModem
 from transceiver import Transceiver
 
 MAX_BATCH = 1 << 16
+PILOT = 64
+
+
+def next_batch(err, bits, act, n_bits_per_sym, n_err_min, bits_sent_max, max_batch=MAX_BATCH, pilot=PILOT):
+    """Trials of the next batch of one grid point under the reference's stopping rule
+    (mp_model.py:137-138,177-187: a counter stays open while n_err < n_err_min and
+    bits < bits_sent_max; all counters share the trials).  ``act`` marks the open counters.
+
+    Never crosses ``bits_sent_max`` of the most advanced open counter.  Before any error
+    is seen, a pilot batch; then the trials the slowest open counter needs to reach
+    ``n_err_min`` at its observed rate, +5 %."""
+    err = np.asarray(err, dtype=np.float64)
+    bits = np.asarray(bits, dtype=np.float64)
+    act = np.asarray(act, dtype=bool)
+    open_bits = bits[act] if act.any() else bits
+    budget = max(1, int(np.ceil((bits_sent_max - float(np.max(open_bits))) / n_bits_per_sym)))
+    need = 0
+    for e, b in zip(err[act], bits[act]):
+        if e <= 0 or b <= 0:
+            need = max(need, max(pilot, int(2 * b / n_bits_per_sym)))  # no rate yet: pilot / doubling
+        else:
+            rate = e / (b / n_bits_per_sym)  # errors per trial
+            need = max(need, int(np.ceil(1.05 * (n_err_min - e) / rate)) + 1)
+    return int(max(1, min(max_batch, budget, max(need, min(pilot, budget)))))
 
 
 def _seed64(seed_arr) -> int:
@@ -174,10 +204,8 @@ class Link:
             run_iters = [int(iters_all[i]) for i in order if flags[i]]
             if not run_iters:  # only the clean counter is still open: the engine always runs iteration 0
                 run_iters, idx = [0], []
-            # one batch never crosses bits_sent_max of the most advanced open counter
-            open_bits = bits[act] if act.any() else bits
-            remaining = max(1.0, self.bits_sent_max - float(np.max(open_bits)))
-            n = int(min(self.max_batch, max(1, np.ceil(remaining / self.n_bits_per_ofdm_sym))))
+            n = next_batch(err, bits, act, self.n_bits_per_ofdm_sym, self.n_err_min, self.bits_sent_max,
+                           self.max_batch)
             uniq = sorted(set(run_iters))
             e, b, _ = eng.run(seed, trial, n, uniq, clean_on)
             trial += n
@@ -195,6 +223,47 @@ class Link:
             finally:
                 if lock:
                     lock.release()
+
+    def simulate_points(self, incl_clean_run: bool, reroll_chan: bool, cnc_n_iter_lst, seed_arrs, point_params,
+                        n_err, n_bits) -> None:
+        """``simulate`` for many grid points of this system at once (the drivers' grid loops,
+        main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:100-215): every round launches one
+        batch of every still-open point (mimo_engine_run_points); the counters of point i
+        (``n_err[i]``, ``n_bits[i]``: float arrays [n_idx], added to) follow the same stopping
+        rule and batch sizes as ``simulate`` would give them, so the totals are bit-identical.
+        ``point_params[i]`` is ``point_params()`` captured at point i (after
+        update_distortion / set_snr)."""
+        eng = self.engine(reroll_chan)
+        P = len(point_params)
+        iters_all = np.asarray(cnc_n_iter_lst, dtype=np.int64).reshape(-1)
+        uniq = sorted(set(int(i) for i in iters_all))
+        res_idx = 1 if incl_clean_run else 0
+        col = np.asarray([res_idx + uniq.index(int(i)) for i in iters_all], dtype=np.int64)  # counter -> engine column
+        if incl_clean_run:
+            col = np.concatenate(([0], col))
+        seeds = [_seed64(s) for s in seed_arrs]
+        trial = np.zeros(P, dtype=np.int64)
+        n_err = np.asarray(n_err)
+        n_bits = np.asarray(n_bits)
+        while True:
+            todo = []
+            for i in range(P):
+                act = (n_err[i] < self.n_err_min) & (n_bits[i] < self.bits_sent_max)
+                if act.any():
+                    todo.append((i, act, next_batch(n_err[i], n_bits[i], act, self.n_bits_per_ofdm_sym,
+                                                    self.n_err_min, self.bits_sent_max, self.max_batch)))
+            if not todo:
+                break
+            for pp in point_params:
+                if pp["snr_db"] is None:
+                    raise ValueError("set_snr() must be called before simulate_points()")
+            e, b, _ = eng.run_points([point_params[i] for i, _, _ in todo], [seeds[i] for i, _, _ in todo],
+                                     [int(trial[i]) for i, _, _ in todo], [n for _, _, n in todo], uniq,
+                                     incl_clean_run)
+            for j, (i, act, n) in enumerate(todo):
+                n_err[i, act] += e[j, col[act]].astype(np.float64)
+                n_bits[i, act] += b[j, col[act]].astype(np.float64)
+                trial[i] += n
 
     def update_distortion(self, ibo_val_db: float) -> None:
         """(mp_model.py:230-241)"""

@@ -6,9 +6,11 @@ Replaces the outer loops of the reference drivers (e.g.
 on one host with ``num_cores`` forked ``Link.simulate`` processes and shared counters.
 
 MI355X design: one process per GPU (torchrun; ``torch.distributed`` with the ``nccl``
-backend = RCCL over xGMI).  Grid points are independent, so they are dealt round-robin
-over ranks with no data-path communication; each point's Philox seed is derived from its
-grid index, so results do not depend on the number of GPUs.  The only collective is one
+backend = RCCL over xGMI).  Grid points are independent, so they are dealt over ranks by
+estimated cost (LPT) with no data-path communication; each point's Philox seed is derived
+from its grid index, so results do not depend on the number of GPUs.  On a rank, all its
+points run together (``Link.simulate_points``: one kernel launch per stopping-rule round
+covers every open point, so a grid of ~400-trial points fills the GPU).  The only collective is one
 all-reduce of the int64 counter tensor [points, indices, {errors, bits}] at the end (a
 few KB: latency-bound, one message).  Rank 0 then forms BERs and writes the reference's
 CSV layouts (``docs/source/usage.rst:40-56``).
@@ -31,16 +33,54 @@ def point_seed(base_seed: int, point_index: int) -> list:
     return [int(base_seed) & 0x7FFFFFFFFFFFFFFF, int(point_index), 0x5EED]
 
 
-def owned_points(n_points: int, rank: int, world: int) -> list:
-    return list(range(rank, n_points, world))
+def owned_points(n_points: int, rank: int, world: int, costs=None) -> list:
+    """Grid points of ``rank``: longest-processing-time-first over the estimated costs
+    (every rank computes the same deterministic assignment); round-robin without costs."""
+    if costs is None:
+        return list(range(rank, n_points, world))
+    load = [0.0] * world
+    mine = []
+    for p in sorted(range(n_points), key=lambda i: (-float(costs[i]), i)):
+        r = min(range(world), key=lambda k: (load[k], k))
+        load[r] += float(costs[p])
+        if r == rank:
+            mine.append(p)
+    return sorted(mine)
+
+
+def point_costs(ibo_arr, ebn0_arr, n_bits_per_sym, constel_size, n_err_min, bits_sent_max, iters, n_ant=64,
+                is_mcnc=False):
+    """Relative cost of every (IBO, Eb/N0) point for sharding: expected trials x cost per trial.
+
+    Trials: a point runs until its best counter has n_err_min errors or the bit budget is
+    spent (mp_model.py:177-187); the best counter's BER is estimated by Gray-QAM over AWGN
+    at the point's Eb/N0 (a lower bound: clipping only adds errors), so low-SNR points are
+    cheap and high-SNR points hit bits_sent_max.  Per trial: one array pass (n_ant FFT pairs)
+    plus one FFT pair per CNC iteration, or one more array pass per MCNC iteration."""
+    from scipy import special
+    M = float(constel_size)
+    k = np.log2(M)
+    budget = bits_sent_max / n_bits_per_sym
+    max_it = int(np.max(iters)) if len(iters) else 0
+    per_trial = n_ant * (1 + max_it) if is_mcnc else n_ant + max_it
+    out = np.zeros(len(ibo_arr) * len(ebn0_arr))
+    for i in range(len(ibo_arr)):
+        for j, e in enumerate(ebn0_arr):
+            g = 10 ** (e / 10)
+            ber = 2 / k * (1 - 1 / np.sqrt(M)) * special.erfc(np.sqrt(1.5 * k * g / (M - 1)))
+            trials = min(budget, n_err_min / max(ber * n_bits_per_sym, 1e-30))
+            out[i * len(ebn0_arr) + j] = max(trials, 1.0) * per_trial
+    return out
 
 
 def run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean=True, seed=2137, rank=0, world=1, dist=None,
-             device=None, reroll_chan=True):
+             device=None, reroll_chan=True, multipoint=True):
     """Simulate every (IBO, Eb/N0) point this rank owns; all-reduce the counters.
 
     Returns (err, bits) int64 arrays of shape [n_ibo, n_ebn0, n_idx] on every rank.
-    ``link`` is a ``mp_model.Link``-like object (update_distortion / set_snr / simulate).
+    ``link`` is a ``mp_model.Link``-like object (update_distortion / set_snr / simulate;
+    with ``simulate_points`` all owned points run together, a few launches per grid).
+    Points are dealt by estimated cost (``point_costs``, LPT).
     """
     ibo_arr = np.asarray(ibo_arr, dtype=np.float64)
     ebn0_arr = np.asarray(ebn0_arr, dtype=np.float64)
@@ -49,19 +89,36 @@ def run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean=True, seed=2137, rank=0,
     n_pts = len(ibo_arr) * len(ebn0_arr)
     counts = np.zeros((n_pts, n_idx, 2), dtype=np.int64)
     m = link.my_mod
+    n_bits_sym = int(m.n_sub_carr * np.log2(m.constel_size))
+    costs = point_costs(ibo_arr, ebn0_arr, n_bits_sym, m.constel_size, getattr(link, "n_err_min", 1e5),
+                        getattr(link, "bits_sent_max", 5e6), iters, getattr(link, "n_ant_val", 64),
+                        getattr(link, "is_mcnc", False))
+    mine = owned_points(n_pts, rank, world, costs)
+    batched = multipoint and hasattr(link, "simulate_points")
     current_ibo = None
-    for p in owned_points(n_pts, rank, world):
+    params, seeds = [], []
+    for p in mine:
         i_ibo, i_snr = divmod(p, len(ebn0_arr))
         if current_ibo != ibo_arr[i_ibo]:
             link.update_distortion(ibo_val_db=float(ibo_arr[i_ibo]))
             current_ibo = ibo_arr[i_ibo]
         # drivers convert with n_fft = n_sub_carr (main_mp_miso_cnc_ber_vs_ebn0.py:112)
         link.set_snr(float(ebn0_to_snr(ebn0_arr[i_snr], m.n_sub_carr, m.n_sub_carr, m.constel_size)))
+        if batched:
+            params.append(dict(link.point_params()))
+            seeds.append(point_seed(seed, p))
+            continue
         err = np.zeros(n_idx)
         bits = np.zeros(n_idx)
         link.simulate(incl_clean, reroll_chan, iters, point_seed(seed, p), err, bits)
         counts[p, :, 0] = err.astype(np.int64)
         counts[p, :, 1] = bits.astype(np.int64)
+    if batched and mine:
+        err = np.zeros((len(mine), n_idx))
+        bits = np.zeros((len(mine), n_idx))
+        link.simulate_points(incl_clean, reroll_chan, iters, seeds, params, err, bits)
+        counts[mine, :, 0] = err.astype(np.int64)
+        counts[mine, :, 1] = bits.astype(np.int64)
     if dist is not None and world > 1:
         import torch
         dev = torch.device(f"cuda:{device}") if device is not None and dist.get_backend() == "nccl" else None

@@ -1,0 +1,68 @@
+"""Multi-point launches (mimo_engine_run_points) and the config-4 sweep built on them.
+
+* run_points over points with different PA / SNR / seeds / trial ranges gives, per trial,
+  exactly the counts of one mimo_engine_run per point (and of the float64 oracle);
+* sweep.run_grid through Link.simulate_points equals the point-by-point Link.simulate
+  sweep bit-for-bit (same seeds, same stopping-rule batches).
+"""
+import numpy as np
+import pytest
+
+from gpu_util import PRECISIONS, assert_counts_equal, engine_for
+from link_util import build_link
+from oracle import sim
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("prec", PRECISIONS)
+def test_run_points_equals_per_point_runs(prec):
+    cfg = sim.SimConfig(8, 256, 512, 16, ibo_db=1.0, snr_db=12.0)
+    eng = engine_for(cfg, precision=prec)
+    pts, seeds, firsts, ns, refs = [], [], [], [], []
+    for k, (ibo, snr, first, n) in enumerate([(1.0, 12.0, 0, 40), (3.0, 16.0, 7, 1), (0.0, 9.0, 100, 77),
+                                              (5.0, 20.0, 0, 0), (2.0, 14.0, (1 << 32) - 20, 20)]):
+        c = sim.SimConfig(8, 256, 512, 16, ibo_db=ibo, snr_db=snr)
+        e = engine_for(c, precision=prec)
+        pts.append(_point_of(c))
+        seeds.append(1000 + k)
+        firsts.append(first)
+        ns.append(n)
+        _, _, per = e.run(1000 + k, first, n, [0, 1, 3], True, per_trial=True)
+        refs.append(per)
+    err, bits, per = eng.run_points(pts, seeds, firsts, ns, [0, 1, 3], True, per_trial=True)
+    got = np.split(per, np.cumsum(ns)[:-1])
+    for k in range(len(pts)):
+        assert_counts_equal(got[k], refs[k], f"point {k} {prec}")
+        np.testing.assert_array_equal(err[k], refs[k].sum(0))
+        assert np.all(bits[k] == ns[k] * 256 * 4)
+    # and the oracle on the middle point
+    c = sim.SimConfig(8, 256, 512, 16, ibo_db=0.0, snr_db=9.0)
+    ref = sim.run_trials(c, 1002, np.arange(100, 177), iters=[0, 1, 3], incl_clean=True)
+    assert_counts_equal(got[2], ref, f"oracle {prec}")
+
+
+def _point_of(cfg):
+    from oracle.sim import point_params
+    from oracle import refmath as rm
+    pp = point_params(cfg)
+    return dict(ibo_db=cfg.ibo_db, snr_db=cfg.snr_db, avg_symbol_power=pp["es"], pa_kind=cfg.pa,
+                sat_pow=rm.sat_pow(cfg.ibo_db, pp["avg_samp"] / cfg.n_ant), cnc_pa_kind=cfg.pa,
+                cnc_sat_pow=pp["cnc_sat"], cnc_alpha=pp["cnc_alpha"])
+
+
+@pytest.mark.parametrize("receiver", ["cnc", "mcnc"])
+def test_multipoint_sweep_equals_sequential(receiver):
+    import sweep
+    kw = dict(n_ant=8, n_sc=256, n_fft=512, M=16, bits_sent_max=1024 * 300, n_err_min=2000,
+              is_mcnc=receiver == "mcnc")
+    ibo, ebn0 = [0.0, 1.5, 4.0], [4.0, 8.0, 12.0, 30.0]
+    link, _ = build_link(**kw)
+    err, bits = sweep.run_grid(link, ibo, ebn0, [0, 1, 2], False, seed=5)
+    link2, _ = build_link(**kw)
+    err2, bits2 = sweep.run_grid(link2, ibo, ebn0, [0, 1, 2], False, seed=5, multipoint=False)
+    np.testing.assert_array_equal(err, err2)
+    np.testing.assert_array_equal(bits, bits2)
+    # the stopping rule: every counter closed by errors or the budget
+    assert np.all((err >= 2000) | (bits >= 1024 * 300))
+    assert np.all(bits <= 1024 * 300 + 64 * 1024)  # overshoot of at most one pilot batch

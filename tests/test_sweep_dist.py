@@ -95,3 +95,13 @@ def test_published_csv_layout_readable():
     d = os.path.join(os.path.dirname(__file__), "golden")
     rows = utilities.read_from_csv("published_ber_vs_ebn0_cnc_rayleigh_ibo3", directory=d)
     assert rows[0][0] == 5.0 and len(rows) == 11 and len(rows[1]) == 16
+
+
+def test_sweep_shards_cover_and_balance():
+    import sweep
+    costs = sweep.point_costs(np.arange(0, 8, 0.5), np.arange(10, 22.1, 0.5), 12288, 64, 1e5, 5e6, range(9))
+    for world in (1, 2, 3, 8):
+        parts = [sweep.owned_points(len(costs), r, world, costs) for r in range(world)]
+        assert sorted(p for q in parts for p in q) == list(range(len(costs)))
+        loads = [costs[q].sum() for q in parts]
+        assert max(loads) <= min(loads) + costs.max()

@@ -1,0 +1,147 @@
+"""BASELINE config 4 on the GPU against the reference's published fixed-BER grids.
+
+Runs ``sweep.run_grid`` exactly as the reference's fixed-BER driver sets up its grid
+(main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:100-215: 64-antenna ULA, N_fft 4096,
+2048 sub-carriers, 64-QAM, soft limiter, IBO 0..7.5 dB x Eb/N0 10..22 dB in 0.5 dB steps,
+receiver iterations 0..8, no clean run, bits_sent_max 5e6, n_err_min 1e5) and compares
+every (IBO, Eb/N0, iteration) BER with the published CSV
+(tests/golden/published_fixed_ber1.0e-02_<rx>_<channel>_nant64_...csv, a data file of the
+reference's figs/csv_results) by a z-score.
+
+sigma: batch means.  The per-trial dispersion of every (point, iteration) is measured from
+a separate per-trial sample (``n_disp`` trials per point, run_points per_trial=True); the
+GPU estimate's sigma = dispersion / sqrt(trials run), the published estimate's sigma =
+dispersion / sqrt(trials the reference ran), where the reference's trial count follows its
+stopping rule from the published BERs (all counters share trials; a counter closes at
+n_err_min errors or the bit budget).
+
+    python tools/fixed_ber_check.py --channel rayleigh --receiver cnc [--precision f64]
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (REPO, os.path.join(REPO, "m-mimo-ofdm-with-nonlinear-pa-sim_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+IBO = np.arange(0.0, 8.0, 0.5)
+EBN0 = np.arange(10.0, 22.1, 0.5)
+ITERS = np.arange(0, 9)
+N_ANT, N_SC, N_FFT, M, CP = 64, 2048, 4096, 64, 128
+BITS_MAX, N_ERR_MIN = int(5e6), int(1e5)
+
+
+def published(channel, receiver):
+    import utilities
+    name = ("published_fixed_ber1.0e-02_%s_%s_nant64_ebn0_min10_max22_step0.50_ibo_min0_max7_step0.50_"
+            "niter1_2_3_4_5_6_7_8" % (receiver, channel))
+    rows = utilities.read_from_csv(name, directory=GOLDEN)
+    ibo = np.asarray(rows[0], dtype=np.float64)
+    ber = np.asarray(rows[1:], dtype=np.float64).reshape(len(ibo), -1, len(ITERS))
+    return ibo, ber
+
+
+def build_link(channel, receiver, precision):
+    import antenna_array
+    import channel as ch_mod
+    import distortion
+    import modulation
+    import mp_model
+    import noise
+    import transceiver
+    mod = modulation.OfdmQamModem(constel_size=M, n_fft=N_FFT, n_sub_carr=N_SC, cp_len=CP)
+    dist = distortion.SoftLimiter(0, mod.avg_sample_power)
+    tx = transceiver.Transceiver(modem=copy.deepcopy(mod), impairment=copy.deepcopy(dist), center_freq=int(3.5e9),
+                                 carrier_spacing=int(15e3))
+    rx = transceiver.Transceiver(modem=copy.deepcopy(mod), impairment=copy.deepcopy(dist), cord_x=212, cord_y=212,
+                                 cord_z=1.5, center_freq=int(3.5e9), carrier_spacing=int(15e3))
+    arr = antenna_array.LinearArray(n_elements=N_ANT, base_transceiver=tx, center_freq=int(3.5e9),
+                                    wav_len_spacing=0.5, cord_x=0, cord_y=0, cord_z=15)
+    if channel == "rayleigh":
+        ch = ch_mod.MisoRayleighFd(tx_transceivers=arr.array_elements, rx_transceiver=rx, seed=1234)
+    else:
+        ch = ch_mod.MisoLosFd() if channel == "los" else ch_mod.MisoTwoPathFd()
+        ch.calc_channel_mat(tx_transceivers=arr.array_elements, rx_transceiver=rx, skip_attenuation=False)
+    return mp_model.Link(mod_obj=mod, array_obj=arr, std_rx_obj=rx, chan_obj=ch, noise_obj=noise.Awgn(snr_db=10),
+                         rx_loc_var=10.0, n_err_min=N_ERR_MIN, bits_sent_max=BITS_MAX, is_mcnc=receiver == "mcnc",
+                         precision=precision)
+
+
+def reference_trials(pub_ber, bits_per_sym):
+    """Trials the reference's stopping rule needed per point: every counter closes at
+    n_err_min errors or at the bit budget; the point stops when all are closed."""
+    budget = BITS_MAX / bits_per_sym
+    need = np.where(pub_ber > 0, N_ERR_MIN / np.maximum(pub_ber, 1e-300) / bits_per_sym, budget)
+    return np.minimum(budget, np.ceil(need.max(axis=-1)))
+
+
+def run(channel="rayleigh", receiver="cnc", precision="f64", n_disp=32, seed=2137):
+    import sweep
+    from utilities import ebn0_to_snr
+    link = build_link(channel, receiver, precision)
+    bits_per_sym = N_SC * int(np.log2(M))
+    t0 = time.perf_counter()
+    err, bits = sweep.run_grid(link, IBO, EBN0, ITERS, incl_clean=False, seed=seed)
+    wall = time.perf_counter() - t0
+    trials = bits[..., 0] / bits_per_sym
+    ber = err / bits
+    # per-trial dispersion sample (independent trial indices)
+    eng = link.engine()
+    params = []
+    for i in IBO:
+        link.update_distortion(float(i))
+        for e in EBN0:
+            link.set_snr(float(ebn0_to_snr(e, N_SC, N_SC, M)))
+            params.append(dict(link.point_params()))
+    P = len(params)
+    from mp_model import _seed64
+    seeds = [_seed64(sweep.point_seed(seed + 1, p)) for p in range(P)]
+    _, _, per = eng.run_points(params, seeds, [0] * P, [n_disp] * P, [int(x) for x in ITERS], False, per_trial=True)
+    per = per.reshape(len(IBO), len(EBN0), n_disp, len(ITERS)).astype(np.float64) / bits_per_sym
+    disp = per.std(axis=2, ddof=1)                       # per-trial BER dispersion
+    disp = np.maximum(disp, np.sqrt(np.maximum(ber, 1e-12) / bits_per_sym))  # floor: binomial
+    pub_ibo, pub = published(channel, receiver)
+    assert np.allclose(pub_ibo, IBO) and pub.shape == ber.shape, (pub_ibo, pub.shape, ber.shape)
+    n_ref = reference_trials(pub, bits_per_sym)[..., None]
+    sig = disp * np.sqrt(1.0 / trials[..., None] + 1.0 / n_ref)
+    sel = pub >= 1e-3
+    z = np.where(sel, (ber - pub) / sig, 0.0)
+    rel = np.where(sel, np.abs(ber - pub) / np.maximum(pub, 1e-300), 0.0)
+    worst = np.unravel_index(np.argmax(np.abs(z)), z.shape)
+    n_sym = int(trials.sum())
+    out = dict(channel=channel, receiver=receiver, precision=precision, points=int(P), ofdm_symbols=n_sym,
+               wall_s=round(wall, 3), symbols_per_s=round(n_sym / wall, 1), compared=int(sel.sum()),
+               max_abs_z=round(float(np.abs(z).max()), 3), mean_z2=round(float((z[sel] ** 2).mean()), 3),
+               frac_abs_z_gt3=round(float((np.abs(z[sel]) > 3).mean()), 5),
+               median_rel=round(float(np.median(rel[sel])), 5), max_rel=round(float(rel[sel].max()), 4),
+               worst=dict(ibo=float(IBO[worst[0]]), ebn0=float(EBN0[worst[1]]), iteration=int(worst[2]),
+                          ber=float(ber[worst]), published=float(pub[worst]), z=float(z[worst])),
+               trials_per_point=dict(min=int(trials.min()), max=int(trials.max())))
+    return out, ber, pub, z
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--channel", default="rayleigh", choices=["rayleigh", "los", "two_path"])
+    ap.add_argument("--receiver", default="cnc", choices=["cnc", "mcnc"])
+    ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    out, ber, pub, z = run(a.channel, a.receiver, a.precision)
+    print(json.dumps(out), flush=True)
+    if a.out:
+        np.savez(a.out, ber=ber, pub=pub, z=z)
+
+
+if __name__ == "__main__":
+    main()

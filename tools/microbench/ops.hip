@@ -13,11 +13,13 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
   uint32_t a[CHAINS];
   float f[CHAINS];
   float2 p2[CHAINS];
+  double g[CHAINS];
 #pragma unroll
   for (int i = 0; i < CHAINS; ++i) {
     a[i] = seed + threadIdx.x * 7 + i;
     f[i] = (float)(threadIdx.x + i) * 1e-3f;
     p2[i] = make_float2(f[i], f[i] * 0.5f);
+    g[i] = (double)f[i];
   }
   const uint32_t m = 0xD2511F53u + seed;
   for (int it = 0; it < ITERS; ++it) {
@@ -39,11 +41,17 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
       }
       if constexpr (OP == 8) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a[i]) : "s"(m));
       if constexpr (OP == 9) asm volatile("v_mul_hi_u32_u24 %0, %0, %1" : "+v"(a[i]) : "s"(m));
+      if constexpr (OP == 10) asm volatile("v_fma_f64 %0, %0, %0, 1.0" : "+v"(g[i]));
+      if constexpr (OP == 11) asm volatile("v_add_f64 %0, %0, 1.0" : "+v"(g[i]));
+      if constexpr (OP == 12) asm volatile("v_mul_f64 %0, %0, %0" : "+v"(g[i]));
+      if constexpr (OP == 13) asm volatile("v_rsq_f64 %0, %0" : "+v"(g[i]));
+      if constexpr (OP == 14) asm volatile("v_mov_b64 %0, %0" : "+v"(g[i]));
+      if constexpr (OP == 15) asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(g[i]) : "v"(a[i]));
     }
   }
   uint32_t s = 0;
 #pragma unroll
-  for (int i = 0; i < CHAINS; ++i) s += a[i] + __float_as_uint(f[i]) + __float_as_uint(p2[i].y);
+  for (int i = 0; i < CHAINS; ++i) s += a[i] + __float_as_uint(f[i]) + __float_as_uint(p2[i].y) + (uint32_t)__double2loint(g[i]);
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
@@ -78,6 +86,12 @@ int main() {
   run<7>("v_pk_fma_f32", d, grid);
   run<0>("v_mul_hi_u32", d, grid);
   run<1>("v_mul_lo_u32", d, grid);
+  run<10>("v_fma_f64", d, grid);
+  run<11>("v_add_f64", d, grid);
+  run<12>("v_mul_f64", d, grid);
+  run<13>("v_rsq_f64", d, grid);
+  run<14>("v_mov_b64", d, grid);
+  run<15>("v_cvt_f64_u32", d, grid);
   run<2>("v_mad_u64_u32(+xor)", d, grid);
   run<8>("v_mul_u32_u24", d, grid);
   run<9>("v_mul_hi_u32_u24", d, grid);
