@@ -238,7 +238,7 @@ struct TeamFft {
   // fp64 elements are 16 B (ds_write_b128: 8-lane groups over 32 banks), where stage 0's
   // stride-R writes need one pad slot per 8 elements: the modelled extra LDS cycles of
   // exchange 0 drop 3x (tools/lds_conflicts.py; the model reproduces SQ_LDS_BANK_CONFLICT
-  // of the 1/16 layout exactly, profiles/r02/abl64).  F = 8192 keeps 1/16: its 16 KiB
+  // of the 1/16 layout exactly, profiles/r02/pmc_f64_r1).  F = 8192 keeps 1/16: its 16 KiB
   // more would not fit the 160 KiB LDS next to the fp64 tables and the CSI scratch.
   static constexpr int PAD0 = (sizeof(Re) == 8 && F < 8192) ? 3 : MIMO_PAD0_SHIFT;
   static constexpr int psh(int S) { return S == 0 ? PAD0 : MIMO_PADN_SHIFT; }
@@ -352,8 +352,10 @@ struct TeamFft {
   static constexpr int kMaxB = 5;
   // Measured -1.1 % (F 2048), -1.5 % (F 4096), +0.9 % (F 8192: more stages held live).
   // fp64: off (the prefetched twiddles would hold ~32 more VGPRs across a transform).
+  // fp64: -2.4 % at F = 2048 (with the channel pipeline off, below), +1.5 % at F = 4096
+  // (profiles/r02/ab/ab64_*.json).
 #ifndef MIMO_TW_PREFETCH64
-#define MIMO_TW_PREFETCH64 0
+#define MIMO_TW_PREFETCH64 (F <= 2048)
 #endif
   static constexpr bool PREFETCH = MIMO_TW_PREFETCH && F <= 4096 && (sizeof(Re) == 4 || MIMO_TW_PREFETCH64);
   // Base holds w(2^k) for k < kMaxB; a stage reads k < bits(S) <= LOG_P.

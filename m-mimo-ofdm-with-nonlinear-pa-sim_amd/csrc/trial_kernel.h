@@ -672,7 +672,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     for (int s = 0; s < NSLOT; ++s) acc[s] = czero<R>();
     // Software pipeline (PIPE): antenna a+1's channel draws (one Philox call per chunk)
     // run inside antenna a's FFT exchanges, where the wave otherwise waits on LDS.
-    constexpr bool PIPE = MIMO_HPIPE && ALIGNED && CH == CH_RAYLEIGH && !CSI;
+    // fp64 at F <= 2048: off (the pipelined draws' registers cost more than the exchange
+    // windows hide: -1.8 % without, profiles/r02/ab/ab64_2048.json).
+    constexpr bool PIPE = MIMO_HPIPE && ALIGNED && CH == CH_RAYLEIGH && !CSI && !(sizeof(R) == 8 && F <= 2048);
     C hnext[PIPE ? NSLOT : 1];
     if constexpr (PIPE) {
       const R sa = p.ant_rel[0];

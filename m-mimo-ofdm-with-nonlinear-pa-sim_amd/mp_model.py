@@ -27,6 +27,9 @@ from __future__ import annotations
 
 import copy
 import multiprocessing
+import os
+import tempfile
+import time
 
 import numpy as np
 from numpy import ndarray
@@ -72,13 +75,66 @@ def _seed64(seed_arr) -> int:
     return int(w[0]) | (int(w[1]) << 32)
 
 
+def _device_count():
+    """GPUs visible to this process, counted without creating a HIP context where possible
+    (torch's counter does not initialise the GPU on ROCm; the HIP runtime is the fallback)."""
+    env = os.environ.get("MIMO_DEVICE_COUNT")
+    if env:
+        return int(env)
+    try:
+        import torch
+        n = torch.cuda.device_count()
+        if n > 0:
+            return n
+    except Exception:  # torch absent or without ROCm: ask the engine library
+        pass
+    return _engine.lib().mimo_device_count()
+
+
 def _default_device():
     """Device for this process: mp child k -> GPU k % n (drivers fork one Link per core)."""
     ident = getattr(multiprocessing.current_process(), "_identity", ())
-    n = _engine.lib().mimo_device_count()
+    n = _device_count()
     if n < 1:
         raise _engine.EngineError("no HIP device visible")
     return (ident[0] - 1) % n if ident else 0
+
+
+# ---------------------------------------------------------------- engines per device
+# The reference's drivers fork num_cores = mp.cpu_count() workers per grid point
+# (main_mp_miso_cnc_ber_vs_ebn0.py:36,124-132); on a many-core MI355X host an unmodified
+# driver would open dozens of HIP contexts per GPU.  A worker therefore takes one of
+# MIMO_MAX_ENGINES_PER_DEVICE (default 2) slots of its device before it creates an engine:
+# POSIX record locks on per-(device, slot) files, held by the process (released when it
+# exits, never inherited by fork children).  Workers without a slot wait, touching no GPU,
+# and return as soon as the shared counters say the point is done.
+_SLOTS = {}  # (pid, device) -> fd of the held slot
+
+
+def _slot_dir():
+    d = os.environ.get("MIMO_LOCK_DIR") or os.path.join(tempfile.gettempdir(), "mimo_engine_slots_%d" % os.getuid())
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def acquire_device_slot(dev: int) -> bool:
+    """Take (or confirm) this process's engine slot on ``dev``; False if all are taken."""
+    import fcntl
+    key = (os.getpid(), int(dev))
+    if key in _SLOTS:
+        return True
+    cap = max(1, int(os.environ.get("MIMO_MAX_ENGINES_PER_DEVICE", "2")))
+    d = _slot_dir()
+    for k in range(cap):
+        fd = os.open(os.path.join(d, "dev%d_slot%d.lock" % (dev, k)), os.O_RDWR | os.O_CREAT, 0o600)
+        try:
+            fcntl.lockf(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
+        except OSError:
+            os.close(fd)
+            continue
+        _SLOTS[key] = fd
+        return True
+    return False
 
 
 class Link:
@@ -140,6 +196,7 @@ class Link:
             raise NotImplementedError("a fixed Rayleigh realisation (reroll_chan=False) is not supported: "
                                       "the engine draws every trial's channel on the device")
         dev = self.device if self.device is not None else _default_device()
+        acquire_device_slot(dev)  # best effort here; simulate() waits for a slot
         key = (dev, kind, bool(reroll_chan), self.is_mcnc, self.precision)
         if self._engine is None or self._engine_key != key:
             m = self.my_mod
@@ -185,12 +242,25 @@ class Link:
     def simulate(self, incl_clean_run: bool, reroll_chan: bool, cnc_n_iter_lst: list, seed_arr: list,
                  n_err_shared_arr, n_bits_sent_shared_arr) -> None:
         """Monte-Carlo trial loop on the GPU (mp_model.py:89-228)."""
+        err_np = np.frombuffer(n_err_shared_arr.get_obj()) if hasattr(n_err_shared_arr, "get_obj") else None
+
+        def still_open():
+            err = np.asarray(err_np if err_np is not None else n_err_shared_arr[:], dtype=np.float64)
+            bits = np.asarray(n_bits_sent_shared_arr[:], dtype=np.float64)
+            return bool(np.any((err < self.n_err_min) & (bits < self.bits_sent_max)))
+
+        dev = self.device if self.device is not None else _default_device()
+        while not acquire_device_slot(dev):  # the device has its engines: wait, no GPU use
+            if not still_open():
+                return
+            time.sleep(0.02)
+        if not still_open():  # a slot freed because its holder finished the point
+            return
         eng = self.engine(reroll_chan)
         seed = _seed64(seed_arr)
         iters_all = np.asarray(cnc_n_iter_lst, dtype=np.int64).reshape(-1)
         order = np.argsort(iters_all, kind="stable")
         res_idx = 1 if incl_clean_run else 0
-        err_np = np.frombuffer(n_err_shared_arr.get_obj()) if hasattr(n_err_shared_arr, "get_obj") else None
         trial = 0
         while True:
             err = np.asarray(err_np if err_np is not None else n_err_shared_arr[:], dtype=np.float64)
@@ -257,9 +327,15 @@ class Link:
             for pp in point_params:
                 if pp["snr_db"] is None:
                     raise ValueError("set_snr() must be called before simulate_points()")
+            t0 = time.perf_counter()
             e, b, _ = eng.run_points([point_params[i] for i, _, _ in todo], [seeds[i] for i, _, _ in todo],
                                      [int(trial[i]) for i, _, _ in todo], [n for _, _, n in todo], uniq,
                                      incl_clean_run)
+            if os.environ.get("MIMO_SWEEP_TRACE"):
+                import sys
+                print("simulate_points round: %d points, %d trials, kernel %.2f ms, call %.2f ms"
+                      % (len(todo), sum(n for _, _, n in todo), eng.kernel_ms, 1e3 * (time.perf_counter() - t0)),
+                      file=sys.stderr)
             for j, (i, act, n) in enumerate(todo):
                 n_err[i, act] += e[j, col[act]].astype(np.float64)
                 n_bits[i, act] += b[j, col[act]].astype(np.float64)

@@ -45,3 +45,37 @@ def simulate_child(link, seed_arr, err, bits, iters=(0, 1)):
     (main_mp_miso_cnc_ber_vs_ebn0.py:122-132)."""
     import numpy as np
     link.simulate(True, True, np.asarray(iters), seed_arr, err, bits)
+
+
+def simulate_child_counting(link, seed_arr, err, bits, created, iters=(0, 1)):
+    """simulate_child, counting the engines this worker creates into ``created`` (an
+    mp.Value): the per-device slot cap must keep the total at MIMO_MAX_ENGINES_PER_DEVICE."""
+    import numpy as np
+
+    import _engine
+    orig = _engine.Engine.__init__
+
+    def counted(self, *a, **k):
+        with created.get_lock():
+            created.value += 1
+        orig(self, *a, **k)
+
+    _engine.Engine.__init__ = counted
+    link.simulate(True, True, np.asarray(iters), seed_arr, err, bits)
+
+
+def sweep_rank(rank, world, port, out, kw, ibo, ebn0, iters):
+    """One rank of a gloo-sharded sweep through the real Link -> engine path (all ranks on
+    GPU 0, as MIMO_BENCH_BACKEND=gloo rehearses bench.py)."""
+    import os
+
+    import numpy as np
+    import torch.distributed as dist
+
+    import sweep
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    link, _ = build_link(device=0, **kw)
+    err, bits = sweep.run_grid(link, ibo, ebn0, iters, False, 11, rank, world, dist)
+    np.save(os.path.join(out, "r%d.npy" % rank), np.stack([err, bits]))
+    dist.destroy_process_group()

@@ -140,3 +140,38 @@ def test_published_curve_paper_config():
         print(e, ber, pub, rel)
         assert np.all(rel < 0.05), (e, ber, pub)
     assert checked >= 40
+
+
+def test_sixteen_workers_share_two_engines(tmp_path, monkeypatch):
+    """An unmodified driver forks one worker per core (main_mp_miso_cnc_ber_vs_ebn0.py:36,
+    124-132).  16 workers on one GPU: at most MIMO_MAX_ENGINES_PER_DEVICE = 2 of them ever
+    create an engine (the others wait without touching the GPU and return when the shared
+    counters close), and the BER matches a single-worker run within sampling error."""
+    import link_util
+    monkeypatch.setenv("MIMO_LOCK_DIR", str(tmp_path))
+    monkeypatch.setenv("MIMO_MAX_ENGINES_PER_DEVICE", "2")
+    ctx = mp.get_context("spawn")
+    per_sym = 256 * 4
+    bmax = per_sym * 4000
+    link, _ = build_link(n_ant=8, n_sc=256, n_fft=512, M=16, ibo=1.0, bits_sent_max=bmax, n_err_min=10 ** 12,
+                         device=0)
+    link.set_snr(14.0)
+    link.max_batch = 256
+    err, bits = ctx.Array(ctypes.c_double, 3, lock=True), ctx.Array(ctypes.c_double, 3, lock=True)
+    created = ctx.Value("i", 0)
+    procs = [ctx.Process(target=link_util.simulate_child_counting, args=(link, [s, 5, 6], err, bits, created))
+             for s in range(16)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert [p.exitcode for p in procs] == [0] * 16
+    print("engines created by 16 workers:", created.value)
+    assert 1 <= created.value <= 2
+    e, b = np.asarray(err[:]), np.asarray(bits[:])
+    assert np.all(b >= bmax) and np.all(b <= bmax + 2 * 256 * per_sym), b
+    err1, bits1 = shared(3)
+    link.simulate(True, True, np.array([0, 1]), [3, 5, 6], err1, bits1)
+    ber, ber1 = e / b, np.asarray(err1[:]) / np.asarray(bits1[:])
+    sig = np.sqrt(ber1 / b) * 4 + 1e-6
+    assert np.all(np.abs(ber - ber1) < 6 * sig), (ber, ber1)

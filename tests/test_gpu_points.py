@@ -66,3 +66,28 @@ def test_multipoint_sweep_equals_sequential(receiver):
     # the stopping rule: every counter closed by errors or the budget
     assert np.all((err >= 2000) | (bits >= 1024 * 300))
     assert np.all(bits <= 1024 * 300 + 64 * 1024)  # overshoot of at most one pilot batch
+
+
+def test_gloo_sharded_sweep_through_real_link_equals_single_process(tmp_path):
+    """world_size 2 over gloo, both ranks on GPU 0, sweep.run_grid through the real
+    Link -> libmimo_engine path: equal to the single-process grid bit-for-bit."""
+    import os
+    import socket
+
+    import torch.multiprocessing as tmp
+
+    import link_util
+    import sweep
+    kw = dict(n_ant=8, n_sc=256, n_fft=512, M=16, bits_sent_max=1024 * 200, n_err_min=3000)
+    ibo, ebn0, iters = [0.0, 2.0, 5.0], [5.0, 9.0, 13.0], [0, 1, 2]
+    link, _ = build_link(device=0, **kw)
+    ref_err, ref_bits = sweep.run_grid(link, ibo, ebn0, iters, False, 11)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    tmp.spawn(link_util.sweep_rank, args=(2, port, str(tmp_path), kw, ibo, ebn0, iters), nprocs=2, join=True)
+    for r in range(2):
+        got = np.load(os.path.join(tmp_path, "r%d.npy" % r))
+        np.testing.assert_array_equal(got[0], ref_err)
+        np.testing.assert_array_equal(got[1], ref_bits)

@@ -58,7 +58,7 @@ def test_point_params_config2():
 
 
 def test_stopping_rule_bits_budget(monkeypatch):
-    link, mod = build_link(bits_sent_max=256 * 40, n_err_min=10 ** 9)
+    link, mod = build_link(bits_sent_max=256 * 40, n_err_min=10 ** 9, device=0)
     fake = FakeEngine(mod.n_bits_per_ofdm_sym)
     monkeypatch.setattr(link, "engine", lambda reroll=True: fake)
     err, bits = shared(1 + 3)
@@ -72,7 +72,7 @@ def test_stopping_rule_bits_budget(monkeypatch):
 
 def test_stopping_rule_per_index(monkeypatch):
     """Indices that reached n_err_min stop accumulating; the others continue (mp_model.py:181-187)."""
-    link, mod = build_link(bits_sent_max=10 ** 9, n_err_min=300, max_batch=16)
+    link, mod = build_link(bits_sent_max=10 ** 9, n_err_min=300, max_batch=16, device=0)
 
     class Skewed(FakeEngine):
         def run(self, seed, first, n, iters, incl_clean, per_trial=False):
@@ -128,3 +128,43 @@ def test_unsupported_channels_raise():
         link._chan_kind = lambda: "rayleigh"
         link.device = 0
         link.engine(reroll_chan=False)
+
+
+def _slot_child(dev, q):
+    import mp_model
+    q.put(mp_model.acquire_device_slot(dev))
+    import time
+    time.sleep(1.0)  # hold the slot while the siblings try
+
+
+def test_device_slots_cap_engines_per_device(tmp_path, monkeypatch):
+    """At most MIMO_MAX_ENGINES_PER_DEVICE processes hold a slot of one device; a slot is
+    per process (re-acquiring is a no-op) and other devices have their own slots."""
+    import mp_model
+    monkeypatch.setenv("MIMO_LOCK_DIR", str(tmp_path))
+    monkeypatch.setenv("MIMO_MAX_ENGINES_PER_DEVICE", "2")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_slot_child, args=(0, q)) for _ in range(5)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=60) for _ in procs]
+    for p in procs:
+        p.join(60)
+    assert sorted(got) == [False, False, False, True, True]
+    # all holders exited: the slots are free again; this process takes one, twice
+    assert mp_model.acquire_device_slot(0) and mp_model.acquire_device_slot(0)
+    assert mp_model.acquire_device_slot(1)
+
+
+def test_waiting_worker_returns_when_point_is_done(tmp_path, monkeypatch):
+    """A worker that finds its device's slots taken never creates an engine; it returns once
+    the shared counters are closed (here: already closed)."""
+    import mp_model
+    monkeypatch.setenv("MIMO_LOCK_DIR", str(tmp_path))
+    monkeypatch.setattr(mp_model, "acquire_device_slot", lambda dev: False)
+    link, _ = build_link(bits_sent_max=1000, n_err_min=10, device=0)
+    monkeypatch.setattr(link, "engine", lambda reroll=True: (_ for _ in ()).throw(AssertionError("engine created")))
+    err, bits = shared(2)
+    err[0] = err[1] = 20.0
+    link.simulate(False, True, np.array([0, 1]), [1], err, bits)

@@ -90,6 +90,7 @@ def run(channel="rayleigh", receiver="cnc", precision="f64", n_disp=32, seed=213
     from utilities import ebn0_to_snr
     link = build_link(channel, receiver, precision)
     bits_per_sym = N_SC * int(np.log2(M))
+    link.engine()  # engine / device set-up outside the timed sweep
     t0 = time.perf_counter()
     err, bits = sweep.run_grid(link, IBO, EBN0, ITERS, incl_clean=False, seed=seed)
     wall = time.perf_counter() - t0
@@ -118,15 +119,25 @@ def run(channel="rayleigh", receiver="cnc", precision="f64", n_disp=32, seed=213
     z = np.where(sel, (ber - pub) / sig, 0.0)
     rel = np.where(sel, np.abs(ber - pub) / np.maximum(pub, 1e-300), 0.0)
     worst = np.unravel_index(np.argmax(np.abs(z)), z.shape)
+    bias = [float(((ber - pub) / np.where(sel, pub, 1.0))[..., i][sel[..., i]].mean()) for i in range(len(ITERS))]
+    req_gpu = sweep.required_ebn0(ber, EBN0, 1e-2)
+    req_pub = sweep.required_ebn0(pub, EBN0, 1e-2)
+    fin = np.isfinite(req_gpu) & np.isfinite(req_pub)
     n_sym = int(trials.sum())
     out = dict(channel=channel, receiver=receiver, precision=precision, points=int(P), ofdm_symbols=n_sym,
                wall_s=round(wall, 3), symbols_per_s=round(n_sym / wall, 1), compared=int(sel.sum()),
-               max_abs_z=round(float(np.abs(z).max()), 3), mean_z2=round(float((z[sel] ** 2).mean()), 3),
+               max_abs_z=round(float(np.abs(z).max()), 3), p95_abs_z=round(float(np.percentile(np.abs(z[sel]), 95)), 3),
+               mean_z2=round(float((z[sel] ** 2).mean()), 3),
+               max_abs_bias_per_iteration=round(float(np.max(np.abs(bias))), 5),
                frac_abs_z_gt3=round(float((np.abs(z[sel]) > 3).mean()), 5),
                median_rel=round(float(np.median(rel[sel])), 5), max_rel=round(float(rel[sel].max()), 4),
                worst=dict(ibo=float(IBO[worst[0]]), ebn0=float(EBN0[worst[1]]), iteration=int(worst[2]),
                           ber=float(ber[worst]), published=float(pub[worst]), z=float(z[worst])),
-               trials_per_point=dict(min=int(trials.min()), max=int(trials.max())))
+               trials_per_point=dict(min=int(trials.min()), max=int(trials.max())),
+               req_ebn0_at_ber_1e2=dict(finite_mismatch=int((np.isfinite(req_gpu) != np.isfinite(req_pub)).sum()),
+                                     compared=int(fin.sum()),
+                                     mean_abs_db=round(float(np.abs(req_gpu - req_pub)[fin].mean()), 4),
+                                     max_abs_db=round(float(np.abs(req_gpu - req_pub)[fin].max()), 4)))
     return out, ber, pub, z
 
 
