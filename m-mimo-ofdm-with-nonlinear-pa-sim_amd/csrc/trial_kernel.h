@@ -690,14 +690,19 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       } else {
         CHN::template gen<FREL>(p, key, trial, a, tl, rx, h);
       }
-      const int an = a + 1 < A ? a + 1 : a;  // the last antenna redraws itself (unused)
+      const int an = a + 1 < A ? a + 1 : a;
       const R san = PIPE ? p.ant_rel[an] : R(0);
       // Window w of NW = 2 XCHG exchange windows (IFFT then FFT) draws chunks
-      // [w NC / NW, (w + 1) NC / NW) of antenna a+1.
+      // [w NC / NW, (w + 1) NC / NW) of antenna a+1.  After the last antenna the draws are
+      // redone for it and unused: a uniform branch around them measured 2.7 % slower (it
+      // splits the exchange windows' basic blocks; profiles/r02/ab/ab32_lastant.json).
+      // Ablation ABL_RNG: antenna a+1's synthetic channel, in window 0.
       auto hfill = [&](int w) __attribute__((always_inline)) {
         if constexpr (PIPE) {
           constexpr int NC = CHN::kChunks, NW = 2 * FFT::XCHG;
-          if (!MIMO_ABL(p, ABL_RNG)) {
+          if (MIMO_ABL(p, ABL_RNG)) {
+            if (w == 0) CHN::template gen<FREL>(p, key, trial, an, tl, rx, hnext);
+          } else {
 #pragma unroll
             for (int c = 0; c < NC; ++c)
               if (c >= w * NC / NW && c < (w + 1) * NC / NW)
@@ -744,7 +749,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       if (!MIMO_ABL(p, ABL_PA)) pa_block(p.pa_kind, d, p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
       if (!MIMO_ABL(p, ABL_FFT)) FFT::template run_second<-1>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_fft);
       if constexpr (PIPE) {
-        if (MIMO_ABL(p, ABL_FFT) || MIMO_ABL(p, ABL_XCHG)) {  // no exchange windows ran
+        if (MIMO_ABL(p, ABL_FFT)) {  // no transforms ran, so no exchange windows (ABL_XCHG keeps them)
 #pragma unroll
           for (int w = 0; w < 2 * FFT::XCHG; ++w) hfill(w);
         }
