@@ -36,17 +36,19 @@ constexpr double kSpeedOfLight = 299792458.0;  // scipy.constants.c
 
 bool is_pow2(long v) { return v > 0 && (v & (v - 1)) == 0; }
 
-// Per-point sums of the per-trial counts of one launch: block (seg, idx) adds the counts of
-// blocks [start[seg], start[seg + 1]) into tot[point_of[seg]][idx] (integer sums: the
-// order does not matter; one 64-bit atomic per wave).
-__global__ void reduce_counts(const uint32_t* __restrict__ c, const uint32_t* __restrict__ start,
+// Per-point sums of the per-trial counts of one launch: block (k, idx) adds the counts of
+// trial blocks [first[k], first[k + 1]) -- a slice of at most kSlice trials of one point --
+// into tot[point_of[k]][idx] (integer sums: the order does not matter; one 64-bit atomic
+// per wave).
+constexpr uint32_t kSlice = 4096;
+__global__ void reduce_counts(const uint32_t* __restrict__ c, const uint32_t* __restrict__ first,
                               const int32_t* __restrict__ point_of, int n_idx, unsigned long long* __restrict__ tot) {
-  const int seg = blockIdx.x, idx = blockIdx.y;
+  const int k = blockIdx.x, idx = blockIdx.y;
   unsigned long long acc = 0;
-  for (uint32_t t = start[seg] + threadIdx.x; t < start[seg + 1]; t += blockDim.x) acc += c[(size_t)t * n_idx + idx];
+  for (uint32_t t = first[k] + threadIdx.x; t < first[k + 1]; t += blockDim.x) acc += c[(size_t)t * n_idx + idx];
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
-  if ((threadIdx.x & 63) == 0) atomicAdd(&tot[(size_t)point_of[seg] * n_idx + idx], acc);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&tot[(size_t)point_of[k] * n_idx + idx], acc);
 }
 
 // Bussgang gain of modulation.py:178-189 as a function of gamma^2.
@@ -150,8 +152,9 @@ struct mimo_engine {
   void* d_points = nullptr;                // TrialParams<R>[segments of one launch]
   size_t points_cap = 0;                   // bytes
   uint32_t* d_start = nullptr;             // [segments + 1] block offsets
-  int32_t* d_point_of = nullptr;           // [segments] point index
-  size_t start_cap = 0, point_of_cap = 0;
+  uint32_t* d_slice_first = nullptr;       // [slices + 1] reduction slices (<= kSlice trials, one point each)
+  int32_t* d_point_of = nullptr;           // [slices] point index
+  size_t start_cap = 0, slice_cap = 0, point_of_cap = 0;
   double d0 = 1.0;
   double last_ms = 0.0;
   std::string desc;
@@ -489,7 +492,9 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
   if (int rc = ensure_cap(e->d_counts, e->counts_cap, (size_t)kChunk * n_idx)) return rc;
   if (int rc = ensure_cap(e->d_tot, e->tot_cap, (size_t)n_points * n_idx)) return rc;
   if (int rc = ensure_cap(e->d_start, e->start_cap, max_seg + 1)) return rc;
-  if (int rc = ensure_cap(e->d_point_of, e->point_of_cap, max_seg)) return rc;
+  const size_t max_slices = max_seg + kChunk / kSlice + 1;
+  if (int rc = ensure_cap(e->d_slice_first, e->slice_cap, max_slices + 1)) return rc;
+  if (int rc = ensure_cap(e->d_point_of, e->point_of_cap, max_slices)) return rc;
   HIP_TRY(hipMemsetAsync(e->d_tot, 0, sizeof(unsigned long long) * n_points * n_idx, e->stream));
   double ms_total = 0.0;
   uint64_t rows_done = 0;
@@ -546,12 +551,17 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
       seg_tab.clear();
       start.assign(1, 0u);
       point_of.clear();
+      std::vector<uint32_t> slice_first(1, 0u);
       for (auto& sg : l) {
         TP q = ptab[sg.point];
         q.first_trial = sg.first;
         seg_tab.push_back(q);
-        start.push_back(start.back() + (uint32_t)sg.n);
-        point_of.push_back(sg.point);
+        const uint32_t b0 = start.back();
+        start.push_back(b0 + (uint32_t)sg.n);
+        for (uint32_t o = 0; o < (uint32_t)sg.n; o += kSlice) {
+          slice_first.push_back(b0 + std::min<uint32_t>((uint32_t)sg.n, o + kSlice));
+          point_of.push_back(sg.point);
+        }
       }
       const uint32_t nb = start.back();
       TP kp = base;
@@ -565,14 +575,16 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
                              e->stream));
       HIP_TRY(hipMemcpyAsync(e->d_point_of, point_of.data(), point_of.size() * sizeof(int32_t),
                              hipMemcpyHostToDevice, e->stream));
+      HIP_TRY(hipMemcpyAsync(e->d_slice_first, slice_first.data(), slice_first.size() * sizeof(uint32_t),
+                             hipMemcpyHostToDevice, e->stream));
       HIP_TRY(hipEventRecord(e->ev0, e->stream));
       bool found = false;
       hipError_t le = launch(key, dim3(nb), e->stream, kp, &found);
       if (!found) return fail(MIMO_ENOKERNEL, std::string("no kernel instance for ") + buf);
       if (le != hipSuccess) return fail(MIMO_EHIP, std::string("trial kernel launch: ") + hipGetErrorString(le));
       HIP_TRY(hipEventRecord(e->ev1, e->stream));
-      hipLaunchKernelGGL(reduce_counts, dim3((unsigned)l.size(), n_idx), dim3(256), 0, e->stream, e->d_counts,
-                         e->d_start, e->d_point_of, n_idx, e->d_tot);
+      hipLaunchKernelGGL(reduce_counts, dim3((unsigned)point_of.size(), n_idx), dim3(256), 0, e->stream,
+                         e->d_counts, e->d_slice_first, e->d_point_of, n_idx, e->d_tot);
       HIP_TRY(hipGetLastError());
       if (per_trial)
         HIP_TRY(hipMemcpyAsync(per_trial + rows_done * n_idx, e->d_counts, (size_t)nb * n_idx * sizeof(uint32_t),
@@ -659,6 +671,7 @@ void mimo_engine_destroy(mimo_engine* e) {
     if (e->d_points) (void)hipFree(e->d_points);
     if (e->d_start) (void)hipFree(e->d_start);
     if (e->d_point_of) (void)hipFree(e->d_point_of);
+    if (e->d_slice_first) (void)hipFree(e->d_slice_first);
     (void)hipEventDestroy(e->ev0);
     (void)hipEventDestroy(e->ev1);
     (void)hipStreamDestroy(e->stream);

@@ -12,7 +12,12 @@ constexpr int team_size(int F) { return F >= 1024 ? F / 16 : 64; }
 // so P = 8 holds the same 32 data registers as the fp32 team's P = 16), one wave below.
 // F = 8192: 16 points per thread (a 1024-thread team would cap the waves at 128 VGPRs;
 // its one 136 KiB exchange buffer allows one team per CU either way).
-constexpr int team_size64(int F) { return F >= 8192 ? F / 16 : F >= 512 ? F / 8 : 64; }
+#ifndef MIMO_F64_P16_MAXF
+#define MIMO_F64_P16_MAXF 0  // A/B knob: fp64 instances with 16 points per thread up to this F
+#endif
+constexpr int team_size64(int F) {
+  return F >= 8192 ? F / 16 : (F <= MIMO_F64_P16_MAXF && F >= 1024) ? F / 16 : F >= 512 ? F / 8 : 64;
+}
 // Alternative team (8 points per thread: half the registers, 2x the waves, one more
 // LDS exchange per transform), selectable with MIMO_TEAM=<T> for A/B measurements.
 constexpr int alt_team_size(int F) { return F >= 1024 ? F / 8 : team_size(F); }
