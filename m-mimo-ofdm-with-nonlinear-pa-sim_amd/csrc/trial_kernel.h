@@ -845,13 +845,15 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     z[s] = mkc((r[s].x + sn * zn[s].x) * ig, (r[s].y + sn * zn[s].y) * ig);
   }
 
-  // ---- CNC / MCNC receiver
+  // ---- CNC / MCNC receiver.  One loop per receiver kind (a uniform branch outside the
+  // loops): the CNC loop then holds neither the MCNC-only state (g, 1/||Hhat||, the
+  // symbols' LDS) nor its code, so it runs without the register spills a shared loop had.
   C dist[NSLOT];
 #pragma unroll
   for (int s = 0; s < NSLOT; ++s) dist[s] = czero<R>();
   int idx = p.incl_clean;
-  for (int it = 0; it <= p.max_iter; ++it) {
-    uint32_t lh[NSLOT];
+  // slice z - dist, count and record iteration `it`; false once the last one is recorded
+  auto detect = [&](int it, uint32_t (&lh)[NSLOT]) __attribute__((always_inline)) -> bool {
     uint32_t errs = 0;
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
@@ -859,8 +861,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       errs += ((valid_mask >> s) & 1u) ? __popc(lh[s] ^ lab[s]) : 0u;
     }
     if ((p.rec_mask >> it) & 1u) record(idx++, errs);
-    if (it == p.max_iter) break;
-    if (p.receiver == RX_CNC) {
+    return it < p.max_iter;
+  };
+  if (p.receiver == RX_CNC) {
+    for (int it = 0;; ++it) {
+      uint32_t lh[NSLOT];
+      if (!detect(it, lh)) break;
       // corrector.py:84-110: single-antenna re-synthesis of the clipping distortion
       C x[NSLOT];
 #pragma unroll
@@ -876,7 +882,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         const C y = SL::gather(d, s, t0);
         dist[s] = ((valid_mask >> s) & 1u) ? csub(cscale(y, sc), qam_point<R>(lh[s], L, hb)) : czero<R>();
       }
-    } else {
+    }
+  } else {
+    // corrector.py:165-207: re-transmit the detected symbols through the whole array
+    for (int it = 0;; ++it) {
+      uint32_t lh[NSLOT];
+      if (!detect(it, lh)) break;
       C est[NSLOT];
       set_symbols(lh);
       array_pass(false, est);
