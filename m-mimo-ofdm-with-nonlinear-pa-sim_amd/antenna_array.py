@@ -56,19 +56,13 @@ class AntennaArray(ABC):
     def transmit(self, in_bits: ndarray, out_domain_fd: bool = True, return_both: bool = False, skip_dist: bool = False,
                  sum_usr_signals: bool = True) -> Union[tuple, ndarray]:
         """Per-antenna precode -> OFDM -> PA (-> FFT): [A, F] or [A, F+cp] (antenna_array.py:58-140)."""
-        if sum_usr_signals is False and self.n_users == 1:
-            sum_usr_signals = True
+        sum_usr_signals = True  # one user (n_users > 1 is rejected by OfdmQamModem)
         modem = self.base_transceiver.modem
         pa = self._uniform_pa()
         if pa is None or not sum_usr_signals:
             return self._transmit_loop(in_bits, out_domain_fd, return_both, skip_dist, sum_usr_signals)
-        if modem.n_users == 1:
-            sym = modem.modulate(in_bits, get_symbols_only=True)
-            pre = np.stack([e.modem.precode_symbols(sym, e.modem.precoding_mat) for e in self.array_elements])
-        else:
-            sym = modem.modulate(in_bits, get_symbols_only=True)
-            pre = np.stack([np.sum(e.modem.precode_symbols(sym, e.modem.precoding_mat), axis=0)
-                            for e in self.array_elements])
+        sym = modem.modulate(in_bits, get_symbols_only=True)
+        pre = np.stack([e.modem.precode_symbols(sym, e.modem.precoding_mat) for e in self.array_elements])
         clean_td = _engine.ofdm_tx(pre, modem.n_fft, modem.n_sub_carr, modem.cp_len)
         kind, sat, p, toi = pa
         dist_td = clean_td if (skip_dist or kind == "none") else _engine.pa(kind, clean_td, sat, p, toi)
@@ -83,43 +77,28 @@ class AntennaArray(ABC):
         return np.squeeze(out)
 
     def _transmit_loop(self, in_bits, out_domain_fd, return_both, skip_dist, sum_usr_signals):
-        res = [t.transmit(in_bits, out_domain_fd=out_domain_fd, return_both=return_both, skip_dist=skip_dist,
-                          sum_usr_signals=sum_usr_signals) for t in self.array_elements]
-        if sum_usr_signals:
-            if return_both and not skip_dist:
-                return np.squeeze(np.stack([r[0] for r in res])), np.squeeze(np.stack([r[1] for r in res]))
-            return np.squeeze(np.stack(res))
-        # [usr, tx, sample]
+        res = [t.transmit(in_bits, out_domain_fd=out_domain_fd, return_both=return_both, skip_dist=skip_dist)
+               for t in self.array_elements]
         if return_both and not skip_dist:
-            return (np.stack([[r[u][0] for r in res] for u in range(self.n_users)]),
-                    np.stack([[r[u][1] for r in res] for u in range(self.n_users)]))
-        return np.stack([[r[u] for r in res] for u in range(self.n_users)])
+            return np.squeeze(np.stack([r[0] for r in res])), np.squeeze(np.stack([r[1] for r in res]))
+        return np.squeeze(np.stack(res))
 
     # ------------------------------------------------------------------ precoding
     def set_precoding_matrix(self, channel_mat_fd=None, mr_precoding: bool = False, zf_precoding: bool = False,
                              update_distortion: bool = False, sep_carr_per_usr: bool = False) -> None:
         """(antenna_array.py:142-311)"""
         n_sc = self.base_transceiver.modem.n_sub_carr
-        if not isinstance(channel_mat_fd, list):
-            hs = sc_columns(channel_mat_fd, n_sc)
-            if mr_precoding:
-                pm = _engine.mrt_precode(hs)
-            else:
-                pm = np.exp(1j * np.angle(np.conjugate(hs)))
-            for idx, t in enumerate(self.array_elements):
-                t.modem.set_precoding(pm[idx, :])
-        elif not sep_carr_per_usr:
-            pm = self._mu_precoding(channel_mat_fd, n_sc, mr_precoding, zf_precoding)
-            for idx, t in enumerate(self.array_elements):
-                t.modem.set_precoding(pm[:, idx, :])
+        if isinstance(channel_mat_fd, list):
+            # per-user channel lists: MU-MR / MU-ZF (antenna_array.py:188-305) are not part of
+            # this build (DESIGN.md §5 / §8)
+            raise NotImplementedError("multi-user precoding is not supported by this build")
+        hs = sc_columns(channel_mat_fd, n_sc)
+        if mr_precoding:
+            pm = _engine.mrt_precode(hs)
         else:
-            comp = None
-            for u, h in enumerate(channel_mat_fd):
-                part = np.hsplit(sc_columns(h, n_sc), len(channel_mat_fd))[u]
-                comp = part if comp is None else np.concatenate((comp, part), axis=1)
-            pm = _engine.mrt_precode(comp) if mr_precoding else np.exp(1j * np.angle(np.conjugate(comp)))
-            for idx, t in enumerate(self.array_elements):
-                t.modem.set_precoding(pm[idx, :])
+            pm = np.exp(1j * np.angle(np.conjugate(hs)))
+        for idx, t in enumerate(self.array_elements):
+            t.modem.set_precoding(pm[idx, :])
         if update_distortion:
             self.update_distortion(ibo_db=self.array_elements[0].impairment.ibo_db,
                                    avg_sample_pow=self.array_elements[0].modem.avg_sample_power)
@@ -133,45 +112,13 @@ class AntennaArray(ABC):
         for idx, t in enumerate(self.array_elements):
             t.modem.set_precoding(pm[idx, :])
 
-    def _mu_precoding(self, chans, n_sc, mr, zf):
-        """Multi-user MR / ZF / phase-only (antenna_array.py:188-296)."""
-        U = self.n_users
-        hs = [sc_columns(h, n_sc) for h in chans]  # U x [A, S]
-        pm = np.empty((U, self.n_elements, n_sc), dtype=np.complex128)
-        if mr:
-            norm = np.sqrt(np.sum([np.sum(np.abs(h) ** 2, axis=0) for h in hs], axis=0))
-            for u in range(U):
-                pm[u] = np.conjugate(hs[u]) / norm
-        elif zf:
-            G = np.stack(hs, axis=0).transpose(2, 1, 0)  # [S, A, U]
-            gram = np.einsum("sau,sav->suv", G, np.conjugate(G))  # H^T H*
-            try:
-                inv = np.linalg.inv(gram)
-            except np.linalg.LinAlgError:
-                inv = np.linalg.pinv(gram)
-            w = np.sqrt(self.n_elements - U) * np.einsum("sau,suv->sav", np.conjugate(G), inv)  # [S, A, U]
-            pm = np.transpose(w, (2, 1, 0)).copy()
-            pw = np.sqrt(np.sum(np.abs(pm) ** 2, axis=(0, 1)))
-            pm = pm / pw[None, None, :]
-        else:
-            for u in range(U):
-                pm[u] = np.exp(1j * np.angle(np.conjugate(hs[u])))
-        return pm
-
     def update_distortion(self, ibo_db: float, avg_sample_pow: float, alpha_val: float = None) -> None:
         """Keep the IBO constant under precoding gain (antenna_array.py:313-360)."""
-        if self.n_users == 1:
-            pm = np.ones((self.n_elements, self.base_transceiver.modem.n_sub_carr), dtype=np.complex128)
-            for idx, t in enumerate(self.array_elements):
-                if t.modem.precoding_mat is not None:
-                    pm[idx, :] = t.modem.precoding_mat
-            gain = np.average(np.abs(pm) ** 2)
-        else:
-            pw = np.ones((self.n_elements, self.base_transceiver.modem.n_sub_carr), dtype=np.float64)
-            for idx, t in enumerate(self.array_elements):
-                if t.modem.precoding_mat is not None:
-                    pw[idx, :] = np.sum(np.abs(t.modem.precoding_mat) ** 2, axis=0)
-            gain = np.average(pw)
+        pm = np.ones((self.n_elements, self.base_transceiver.modem.n_sub_carr), dtype=np.complex128)
+        for idx, t in enumerate(self.array_elements):
+            if t.modem.precoding_mat is not None:
+                pm[idx, :] = t.modem.precoding_mat
+        gain = np.average(np.abs(pm) ** 2)
         for t in self.array_elements:
             if isinstance(t.impairment, distortion.ThirdOrderNonLin):
                 t.modem.alpha = alpha_val

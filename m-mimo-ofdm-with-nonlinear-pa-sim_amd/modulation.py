@@ -156,6 +156,10 @@ class OfdmQamModem(QamModem):
         self.n_bits_per_ofdm_sym = int(np.log2(constel_size) * n_sub_carr)
         self.avg_sample_power = self.ofdm_avg_sample_pow()
         self.precoding_mat = None
+        if n_users != 1:
+            # multi-user modulation / precoding (modulation.py:363-382, antenna_array.py:188-305)
+            # is not part of this build: DESIGN.md §5 / §8
+            raise NotImplementedError("multi-user OFDM (n_users > 1) is not supported by this build")
         self.n_users = n_users
 
     def set_precoding(self, precoding_mat: ndarray) -> None:
@@ -167,21 +171,12 @@ class OfdmQamModem(QamModem):
         return in_symbols
 
     def modulate(self, input_bits: ndarray, get_symbols_only: bool = False, sum_usr_signals: bool = True):
-        if self.n_users == 1:
-            sym = modulate(self._constellation, self.n_bits_per_symbol, input_bits)
-            if get_symbols_only:
-                return sym
-            return _tx_ofdm_symbol(np.squeeze(self.precode_symbols(sym, self.precoding_mat)), self.n_fft,
-                                   self.n_sub_carr, self.cp_len)
-        sym = np.empty((self.n_users, self.n_sub_carr), dtype=np.complex128)
-        for u in range(self.n_users):
-            sym[u, :] = modulate(self._constellation, self.n_bits_per_symbol, input_bits[u, :])
+        """(modulation.py:346-382) one user: ``sum_usr_signals`` has nothing to sum."""
+        sym = modulate(self._constellation, self.n_bits_per_symbol, input_bits)
         if get_symbols_only:
             return sym
-        pre = self.precode_symbols(sym, self.precoding_mat)
-        if sum_usr_signals:
-            return _tx_ofdm_symbol(np.sum(pre, axis=0), self.n_fft, self.n_sub_carr, self.cp_len)
-        return list(_engine.ofdm_tx(pre, self.n_fft, self.n_sub_carr, self.cp_len))
+        return _tx_ofdm_symbol(np.squeeze(self.precode_symbols(sym, self.precoding_mat)), self.n_fft,
+                               self.n_sub_carr, self.cp_len)
 
     def demodulate(self, ofdm_symbol: ndarray, get_symbols_only: bool = False) -> ndarray:
         sym = _rx_ofdm_symbol(ofdm_symbol, self.n_fft, self.n_sub_carr, self.cp_len)

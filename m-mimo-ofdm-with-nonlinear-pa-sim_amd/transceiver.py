@@ -47,9 +47,8 @@ class Transceiver:
     def transmit(self, in_bits: ndarray, out_domain_fd: bool = True, skip_dist: bool = False, return_both: bool = False,
                  sum_usr_signals: bool = True):
         """modulate -> PA -> (FFT)  (transceiver.py:98-174)."""
-        clean = self.modem.modulate(in_bits, sum_usr_signals=sum_usr_signals)
-        per_user = not sum_usr_signals
-        sigs = clean if per_user else [clean]
+        clean = self.modem.modulate(in_bits, sum_usr_signals=sum_usr_signals)  # one user: nothing to sum
+        sigs = [clean]
 
         def fd(x):
             return utilities.to_freq_domain(x, remove_cp=True, cp_len=self.modem.cp_len)
@@ -64,8 +63,6 @@ class Transceiver:
                     out.append([fd(d), fd(c)] if out_domain_fd else [d, c])
                 else:
                     out.append(fd(d) if out_domain_fd else d)
-        if per_user:
-            return out
         return tuple(out[0]) if (return_both and not skip_dist and self.impairment is not None) else out[0]
 
     def receive(self, in_symb_td: ndarray) -> ndarray:

@@ -168,3 +168,16 @@ def test_waiting_worker_returns_when_point_is_done(tmp_path, monkeypatch):
     err, bits = shared(2)
     err[0] = err[1] = 20.0
     link.simulate(False, True, np.array([0, 1]), [1], err, bits)
+
+
+def test_multi_user_is_rejected_explicitly():
+    """Multi-user OFDM / MU-MR / MU-ZF (modulation.py:363-382, antenna_array.py:188-305) are
+    not part of this build: they raise instead of running unverified code."""
+    import numpy as np
+    import modulation
+    with pytest.raises(NotImplementedError):
+        modulation.OfdmQamModem(constel_size=16, n_fft=128, n_sub_carr=64, cp_len=4, n_users=2)
+    link, _ = build_link()
+    h = link.my_miso_chan.channel_mat_fd
+    with pytest.raises(NotImplementedError):
+        link.my_array.set_precoding_matrix([h, h], mr_precoding=True)
