@@ -91,6 +91,21 @@ void fit_alpha(double g0sq, P& p) {
   using R = std::remove_reference_t<decltype(p.apoly[0])>;
   for (int i = 0; i <= D; ++i, sc /= L) p.apoly[i] = (R)(mono[i] * sc);
   p.alpha_xlim = (R)L;
+  // fp64: Chebyshev coefficients of degree 18 on the same interval (Clenshaw in the kernel),
+  // at 64 nodes in long double
+  constexpr int D64 = 18;
+  for (int k = 0; k <= D64; ++k) {
+    long double ck = 0.0L;
+    for (int j = 0; j < N; ++j) {
+      const long double th = 3.14159265358979323846264338327950288L * (j + 0.5L) / N;
+      const long double t = std::cos(th);
+      const long double g2 = (long double)g0sq / (1.0L + (long double)L * t);
+      const long double g = std::sqrt(g2);
+      const long double f = 1.0L - std::exp(-g2) + 0.886226925452758013649083741671L * g * std::erfc(g);
+      ck += f * std::cos(k * th);
+    }
+    p.acheb[k] = (double)(ck * (k == 0 ? 1.0L : 2.0L) / N);
+  }
 }
 
 // fp64 Box-Muller tables (real.h ln_lut / sincos_lut), computed in long double.

@@ -48,8 +48,14 @@ constexpr int kMaxCsiAnt = 512;  // CSI-error runs: antennas (LDS per team; engi
 #ifndef MIMO_ALPHA_POLY
 #define MIMO_ALPHA_POLY 1
 #endif
+#ifndef MIMO_ALPHA_CHEB64
+#define MIMO_ALPHA_CHEB64 1  // fp64: Chebyshev alpha (A/B knob; 0 = library exp / erfc every antenna)
+#endif
 #ifndef MIMO_HPIPE
 #define MIMO_HPIPE 1  // draw antenna a+1's channel inside antenna a's FFT exchanges (aligned Rayleigh)
+#endif
+#ifndef MIMO_HPIPE64_OFF_F
+#define MIMO_HPIPE64_OFF_F 2048  // fp64: no channel pipeline up to this FFT size (A/B knob)
 #endif
 #ifndef MIMO_VK_DPP
 #define MIMO_VK_DPP 1  // per-antenna precoding-power wave sum by DPP (0: __shfl_xor)
@@ -78,6 +84,10 @@ struct TrialParams {
   // fp32 instances only: the fp64 instances always evaluate the exact formula.
   R apoly[9];
   R inv_vk0, alpha_xlim;
+  // fp64 instances: alpha(gamma_a^2) as a Chebyshev series of degree 18 in t = x / alpha_xlim
+  // (Clenshaw; the host fits it at 64 nodes in double: ~1e-16 relative, the singularity of
+  // alpha(g0^2 / (1 + x)) at x = -1 is 4 half-widths away), the exact formula outside.
+  double acheb[19];
   R es_over_snr;                 // Es / 10^(SNR/10)
   R csi_a, csi_b;                // sqrt(1 - eps^2), eps
   R inv_sqrt_f;
@@ -674,7 +684,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     // run inside antenna a's FFT exchanges, where the wave otherwise waits on LDS.
     // fp64 at F <= 2048: off (the pipelined draws' registers cost more than the exchange
     // windows hide: -1.8 % without, profiles/r02/ab/ab64_2048.json).
-    constexpr bool PIPE = MIMO_HPIPE && ALIGNED && CH == CH_RAYLEIGH && !CSI && !(sizeof(R) == 8 && F <= 2048);
+    constexpr bool PIPE = MIMO_HPIPE && ALIGNED && CH == CH_RAYLEIGH && !CSI && !(sizeof(R) == 8 && F <= MIMO_HPIPE64_OFF_F);
     C hnext[PIPE ? NSLOT : 1];
     if constexpr (PIPE) {
       const R sa = p.ant_rel[0];
@@ -768,6 +778,18 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 #pragma unroll
           for (int i = 7; i >= 0; --i) acc = fmar(acc, x, p.apoly[i]);
           alpha_a = acc;
+        } else if (MIMO_ALPHA_CHEB64 && sizeof(R) == 8 && absr(x) <= p.alpha_xlim) {
+          // Clenshaw: b_k = c_k + 2 t b_{k+1} - b_{k+2}; alpha = c_0 + t b_1 - b_2
+          // (~38 f64 ops instead of the library exp + erfc)
+          const double t2 = 2.0 * ((double)x / (double)p.alpha_xlim);
+          double b1 = 0.0, b2 = 0.0;
+#pragma unroll
+          for (int k = 18; k >= 1; --k) {
+            const double b0 = fma(t2, b1, p.acheb[k] - b2);
+            b2 = b1;
+            b1 = b0;
+          }
+          alpha_a = (R)fma(0.5 * t2, b1, p.acheb[0] - b2);
         } else {
           alpha_a = alpha_of_gamma2(p.alpha_c / vks);
         }
