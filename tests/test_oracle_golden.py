@@ -136,3 +136,23 @@ def test_link_end_to_end(name):
             dbg = dd
     np.testing.assert_allclose(dbg["z"], g["z_trial0"], rtol=1e-8, atol=1e-10)
     np.testing.assert_array_equal(np.asarray(counts), g["counts"])
+
+
+@pytest.mark.parametrize("ebn0", [4.0, 8.0])
+def test_config1_siso_awgn_on_cpu_path(ebn0):
+    """BASELINE config 1 on the NumPy CPU path (no GPU): 1 antenna, 64 sub-carriers
+    (FFT 128), 16-QAM, ideal PA (IBO 100 dB), LoS with the RX jitter -- an AWGN link after
+    MRT / AGC.  The BASELINE run is 1e4 bits (40 symbols); 2e5 bits here for a tight check
+    against Gray 16-QAM: BER = 3/8 erfc(sqrt(0.4 Eb/N0))."""
+    from scipy import special
+    from oracle import sim
+    snr = float(sim.rm.ebn0_to_snr(ebn0, 64, 64, 16))
+    cfg = sim.SimConfig(1, 64, 128, 16, pa="softlim", ibo_db=100.0, snr_db=snr, channel="los")
+    counts = sim.run_trials(cfg, 11, np.arange(782), iters=[0], incl_clean=True)  # 782 x 256 bits ~ 2e5
+    bits = 782 * 256
+    ber = counts.sum(0) / bits
+    theory = 3 / 8 * special.erfc(np.sqrt(0.4 * 10 ** (ebn0 / 10)))
+    sigma = np.sqrt(theory * 4 / bits)
+    assert np.all(np.abs(ber - theory) < 5 * sigma), (ber, theory)
+    first40 = sim.run_trials(cfg, 11, np.arange(40), iters=[0])  # the BASELINE 1e4-bit run
+    assert first40.shape == (40, 1) and 0 < first40.sum() < 40 * 256 * 0.2
