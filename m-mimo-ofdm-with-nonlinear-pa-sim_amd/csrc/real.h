@@ -204,6 +204,24 @@ __device__ __forceinline__ void sincos_lut(uint32_t w, double& sn, double& cs) {
   cs = fma(cst.x, c, -(cst.y * s));
 }
 
+// sin / cos of 2 pi r for a double phase r in revolutions (|r| < 2^20), full precision:
+// n = rint(256 r), f = r - n / 256 exactly (Sterbenz), phi = 2 pi f in [-pi/256, pi/256];
+// the series and the table of sincos_lut (LoS / two-path channel phases).  <= ~1.5 ulp.
+__device__ __forceinline__ void sincos_rev_lut(double r, double& sn, double& cs) {
+  const double n = __builtin_rint(256.0 * r);
+  const double phi = (r - n * 0.00390625) * 6.28318530717958647693;
+  const double z = phi * phi;
+  double ps = fma(z, -1.0 / 5040, 1.0 / 120);
+  ps = fma(ps, z, -1.0 / 6);
+  const double s = fma(phi * z, ps, phi);
+  double pc = fma(z, -1.0 / 720, 1.0 / 24);
+  pc = fma(pc, z, -0.5);
+  const double c = fma(z, pc, 1.0);
+  const double2 cst = lut64[kLnTab + ((int)n & 255)];
+  sn = fma(cst.y, c, cst.x * s);
+  cs = fma(cst.x, c, -(cst.y * s));
+}
+
 // sqrt of a positive normal double (no denormal / overflow scaling): v_rsq_f64 seed and
 // the Goldschmidt / Newton refinement of the compiler's lowering.
 __device__ __forceinline__ double sqrt_nr(double x) {

@@ -339,6 +339,17 @@ __device__ __forceinline__ cx<R> qam_point(uint32_t label, int L, int hb) {
 }
 
 // ---------------------------------------------------------------- channel generation
+// sin / cos of a channel phase in revolutions: fp32 hardware (v_sin / v_cos take
+// revolutions), fp64 the table form (real.h sincos_rev_lut; MIMO_SC_LUT = 0: the series).
+__device__ __forceinline__ void sincos_phase(float r, float& sn, float& cs) {
+  sn = sin_rev(r);
+  cs = cos_rev(r);
+}
+__device__ __forceinline__ void sincos_phase(double r, double& sn, double& cs) {
+  if constexpr (MIMO_SC_LUT) sincos_rev_lut(r, sn, cs);
+  else sincos_rev(r, sn, cs);
+}
+
 template <typename R, int F, int T, int NSLOT, bool ALIGNED, int CH>
 struct Channel {
   using SL = Slots<F, T, NSLOT, ALIGNED>;
@@ -503,13 +514,16 @@ struct Channel {
           double ph = d_los * foc;
           ph -= floor(ph);
           const R a1 = att_los * fr;
-          hv = mkc(a1 * cos_rev((R)ph), a1 * sin_rev((R)ph));
+          R sn, cs;
+          sincos_phase((R)ph, sn, cs);
+          hv = mkc(a1 * cs, a1 * sn);
           if constexpr (CH == CH_TWOPATH) {
             double ph2 = d_sec * foc;
             ph2 -= floor(ph2);
             const R a2 = att_sec * fr;
-            hv.x -= a2 * cos_rev((R)ph2);
-            hv.y -= a2 * sin_rev((R)ph2);
+            sincos_phase((R)ph2, sn, cs);
+            hv.x -= a2 * cs;
+            hv.y -= a2 * sn;
           }
         }
         h[s] = hv;
