@@ -39,11 +39,11 @@
 extern "C" {
 #endif
 
-#define MIMO_ABI_VERSION 3
+#define MIMO_ABI_VERSION 4
 
 enum { MIMO_OK = 0, MIMO_EINVAL = -1, MIMO_EHIP = -2, MIMO_ENOKERNEL = -3, MIMO_ENOMEM = -4 };
 enum { MIMO_PA_NONE = 0, MIMO_PA_SOFTLIM = 1, MIMO_PA_RAPP = 2, MIMO_PA_TOI = 3 };
-enum { MIMO_CH_RAYLEIGH = 1, MIMO_CH_LOS = 2, MIMO_CH_TWOPATH = 3 };
+enum { MIMO_CH_RAYLEIGH = 1, MIMO_CH_LOS = 2, MIMO_CH_TWOPATH = 3, MIMO_CH_TABLE = 4 };
 enum { MIMO_RX_CNC = 1, MIMO_RX_MCNC = 2 };
 enum { MIMO_PREC_F64 = 0, MIMO_PREC_F32 = 1 };
 
@@ -56,7 +56,7 @@ typedef struct mimo_config {
   int32_t n_fft;            /* FFT size F: power of two, 128 ... 8192               */
   int32_t constel_size;     /* square QAM order M (4 ... 4096)                      */
   int32_t cp_len;           /* cyclic prefix (BER-neutral: memoryless PA, circular channel) */
-  int32_t channel_kind;     /* MIMO_CH_*                                            */
+  int32_t channel_kind;     /* MIMO_CH_* (TABLE: a fixed matrix, see chan_table)     */
   int32_t receiver_kind;    /* MIMO_RX_*                                            */
   int32_t device;           /* HIP device ordinal, -1 = current                      */
   double rx_pos[3];         /* nominal RX position [m]                               */
@@ -66,6 +66,9 @@ typedef struct mimo_config {
                                float64, modulation.py:270) or MIMO_PREC_F32 (fast variant) */
   const double* tx_pos;     /* [n_ant][3] antenna positions [m]                      */
   const double* carrier_freqs; /* [n_fft] carrier frequencies [Hz] in FFT-bin order  */
+  const double* chan_table; /* MIMO_CH_TABLE only: [n_ant][n_fft] complex channel matrix
+                               (Miso*Fd.channel_mat_fd), the same for every trial -- what
+                               Link.simulate(reroll_chan=False) uses (mp_model.py:190-206) */
 } mimo_config;
 
 /* Grid-point parameters: what Link keeps in its PA / receiver / noise objects. */

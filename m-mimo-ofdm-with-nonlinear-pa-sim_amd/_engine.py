@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MIMO_LIB") or os.path.join(_HERE, "libmimo_engine.so")
 
 PA_KINDS = {"none": 0, "softlim": 1, "rapp": 2, "toi": 3}
-CH_KINDS = {"rayleigh": 1, "los": 2, "two_path": 3}
+CH_KINDS = {"rayleigh": 1, "los": 2, "two_path": 3, "table": 4}
 RX_KINDS = {"cnc": 1, "mcnc": 2}
 # Arithmetic type of the fused kernel: "f64" is the reference's own precision (complex128 /
 # float64, the default); "f32" is the fast variant.  MIMO_PRECISION overrides the default.
@@ -40,7 +40,7 @@ class MimoConfig(ctypes.Structure):
                 ("constel_size", ctypes.c_int32), ("cp_len", ctypes.c_int32), ("channel_kind", ctypes.c_int32),
                 ("receiver_kind", ctypes.c_int32), ("device", ctypes.c_int32), ("rx_pos", ctypes.c_double * 3),
                 ("rx_loc_var", ctypes.c_double), ("reroll_chan", ctypes.c_int32), ("precision", ctypes.c_int32),
-                ("tx_pos", _dp), ("carrier_freqs", _dp)]
+                ("tx_pos", _dp), ("carrier_freqs", _dp), ("chan_table", _dp)]
 
 
 class MimoPoint(ctypes.Structure):
@@ -126,7 +126,7 @@ class Engine:
     """One configured system (the deep-copied objects of a ``Link``) on one GPU."""
 
     def __init__(self, n_ant, n_sub_carr, n_fft, constel_size, cp_len, channel, receiver, tx_pos, rx_pos,
-                 rx_loc_var, carrier_freqs, reroll=True, device=-1, precision=None):
+                 rx_loc_var, carrier_freqs, reroll=True, device=-1, precision=None, chan_table=None):
         L = lib()
         self.precision = precision or default_precision()
         if self.precision not in PRECISIONS:
@@ -135,11 +135,18 @@ class Engine:
         self._fr = _c(carrier_freqs, np.float64)
         if self._tx.shape[0] != n_ant or self._fr.shape[0] != n_fft:
             raise ValueError("tx_pos must be [n_ant, 3] and carrier_freqs [n_fft]")
+        self._tab = None
+        if channel == "table":
+            tab = np.asarray(chan_table, dtype=np.complex128)
+            if tab.shape != (n_ant, n_fft):
+                raise ValueError("chan_table must be the [n_ant, n_fft] channel matrix")
+            self._tab = np.ascontiguousarray(tab).view(np.float64)
         cfg = MimoConfig(n_ant=n_ant, n_sub_carr=n_sub_carr, n_fft=n_fft, constel_size=constel_size, cp_len=cp_len,
                          channel_kind=CH_KINDS[channel], receiver_kind=RX_KINDS[receiver], device=device,
                          rx_loc_var=float(rx_loc_var), reroll_chan=int(bool(reroll)),
                          precision=PRECISIONS[self.precision],
-                         tx_pos=_ptr(self._tx, ctypes.c_double), carrier_freqs=_ptr(self._fr, ctypes.c_double))
+                         tx_pos=_ptr(self._tx, ctypes.c_double), carrier_freqs=_ptr(self._fr, ctypes.c_double),
+                         chan_table=_ptr(self._tab, ctypes.c_double) if self._tab is not None else None)
         cfg.rx_pos[:] = [float(v) for v in rx_pos]
         h = L.mimo_engine_create(ctypes.byref(cfg))
         if not h:

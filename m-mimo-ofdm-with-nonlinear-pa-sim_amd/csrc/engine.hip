@@ -144,6 +144,7 @@ void set_error(const std::string& m) { g_err = m; }
 struct mimo_engine {
   mimo_config cfg{};
   std::vector<double> tx_pos, freqs;
+  std::vector<double> chan_inband;        // MIMO_CH_TABLE: [A][S] (re, im), sub-carrier order k
   mimo_point pt{};
   bool have_point = false;
   // device state (created lazily on the first run: fork safety)
@@ -154,6 +155,8 @@ struct mimo_engine {
   float2* d_tw[2] = {nullptr, nullptr};  // fp32 stage twiddles for team_size(F), alt_team_size(F)
   double2* d_tw64 = nullptr;              // fp64 stage twiddles for team_size64(F)
   double2* d_lut64 = nullptr;             // fp64 Box-Muller tables (lut64_table)
+  float2* d_tab32 = nullptr;              // MIMO_CH_TABLE channel, fp32 / fp64 copies
+  double2* d_tab64 = nullptr;
   float* d_ant_rel = nullptr;
   float* d_f_rel = nullptr;
   double* d_ant_rel64 = nullptr;
@@ -256,8 +259,10 @@ int validate_config(const mimo_config* c) {
   if (L * L != c->constel_size || !is_pow2(c->constel_size) || c->constel_size < 4 || c->constel_size > 4096)
     return fail(MIMO_EINVAL, "Constellation size must be a power of some number, only square QAM supported.");
   if (c->n_ant < 1 || c->n_ant > 4096) return fail(MIMO_EINVAL, "n_ant must be in [1, 4096]");
-  if (c->channel_kind < MIMO_CH_RAYLEIGH || c->channel_kind > MIMO_CH_TWOPATH)
+  if (c->channel_kind < MIMO_CH_RAYLEIGH || c->channel_kind > MIMO_CH_TABLE)
     return fail(MIMO_EINVAL, "unknown channel_kind");
+  if (c->channel_kind == MIMO_CH_TABLE && !c->chan_table)
+    return fail(MIMO_EINVAL, "chan_table is required for MIMO_CH_TABLE");
   if (c->receiver_kind != MIMO_RX_CNC && c->receiver_kind != MIMO_RX_MCNC)
     return fail(MIMO_EINVAL, "unknown receiver_kind");
   if (!c->tx_pos) return fail(MIMO_EINVAL, "tx_pos is required");
@@ -352,7 +357,8 @@ int ensure_device(mimo_engine* e) {
   for (int k = 0; k < S; ++k) {
     const int bin = k < S / 2 ? F - S / 2 + k : k - S / 2 + 1;
     const double f = e->freqs[bin];
-    f_rel64[k] = fc / f;
+    // table channels carry their full attenuation: nothing is factored out of the loops
+    f_rel64[k] = e->cfg.channel_kind == MIMO_CH_TABLE ? 1.0 : fc / f;
     f_rel[k] = (float)f_rel64[k];
     f_over_c[k] = f / kSpeedOfLight;
   }
@@ -376,6 +382,15 @@ int ensure_device(mimo_engine* e) {
   for (int v = 0; v < 2; ++v) {
     HIP_TRY(hipMalloc(&e->d_tw[v], sizeof(float2) * tws[v].size()));
     HIP_TRY(hipMemcpy(e->d_tw[v], tws[v].data(), sizeof(float2) * tws[v].size(), hipMemcpyHostToDevice));
+  }
+  if (!e->chan_inband.empty()) {
+    const size_t n = e->chan_inband.size() / 2;
+    std::vector<float2> t32(n);
+    for (size_t i = 0; i < n; ++i) t32[i] = make_float2((float)e->chan_inband[2 * i], (float)e->chan_inband[2 * i + 1]);
+    HIP_TRY(hipMalloc(&e->d_tab32, sizeof(float2) * n));
+    HIP_TRY(hipMalloc(&e->d_tab64, sizeof(double2) * n));
+    HIP_TRY(hipMemcpy(e->d_tab32, t32.data(), sizeof(float2) * n, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(e->d_tab64, e->chan_inband.data(), sizeof(double2) * n, hipMemcpyHostToDevice));
   }
   const std::vector<double2> lut = lut64_table();
   HIP_TRY(hipMalloc(&e->d_lut64, sizeof(double2) * lut.size()));
@@ -427,6 +442,17 @@ mimo_engine* mimo_engine_create(const mimo_config* cfg) {
   }
   e->cfg.tx_pos = nullptr;
   e->cfg.carrier_freqs = nullptr;
+  if (cfg->channel_kind == MIMO_CH_TABLE) {  // keep the in-band columns, bins b(k) (modulation.py:266-267)
+    const int S = cfg->n_sub_carr;
+    e->chan_inband.resize((size_t)A * S * 2);
+    for (int a = 0; a < A; ++a)
+      for (int k = 0; k < S; ++k) {
+        const int bin = k < S / 2 ? F - S / 2 + k : k - S / 2 + 1;
+        e->chan_inband[((size_t)a * S + k) * 2] = cfg->chan_table[((size_t)a * F + bin) * 2];
+        e->chan_inband[((size_t)a * S + k) * 2 + 1] = cfg->chan_table[((size_t)a * F + bin) * 2 + 1];
+      }
+  }
+  e->cfg.chan_table = nullptr;
   return e;
 }
 
@@ -523,10 +549,12 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
       base.tw = e->d_tw64;
       base.ant_rel = e->d_ant_rel64;
       base.f_rel = e->d_f_rel64;
+      base.chan_tab = e->d_tab64;
     } else {
       base.tw = e->d_tw[key.T == mimo::team_size(c.n_fft) ? 0 : 1];
       base.ant_rel = e->d_ant_rel;
       base.f_rel = e->d_f_rel;
+      base.chan_tab = e->d_tab32;
     }
     base.f_over_c = e->d_f_over_c;
     base.tx_pos = e->d_tx_pos;
@@ -676,6 +704,8 @@ void mimo_engine_destroy(mimo_engine* e) {
     (void)hipFree(e->d_f_rel);
     (void)hipFree(e->d_tw64);
     (void)hipFree(e->d_lut64);
+    if (e->d_tab32) (void)hipFree(e->d_tab32);
+    if (e->d_tab64) (void)hipFree(e->d_tab64);
     (void)hipFree(e->d_f_rel64);
     (void)hipFree(e->d_ant_rel64);
     (void)hipFree(e->d_f_over_c);

@@ -79,6 +79,8 @@ hipError_t by_channel(const InstanceKey& k, dim3 grid, hipStream_t st, const Tri
     case CH_TWOPATH:
       return k.csi ? go<T, NSLOT, AL, CH_TWOPATH, true>(grid, st, p)
                    : go<T, NSLOT, AL, CH_TWOPATH, false>(grid, st, p);
+    case CH_TABLE:
+      return k.csi ? go<T, NSLOT, AL, CH_TABLE, true>(grid, st, p) : go<T, NSLOT, AL, CH_TABLE, false>(grid, st, p);
     default:
       *found = false;
       return hipSuccess;

@@ -34,7 +34,7 @@
 namespace mimo {
 
 enum PaKind : int { PA_NONE = 0, PA_SOFTLIM = 1, PA_RAPP = 2, PA_TOI = 3 };
-enum ChanKind : int { CH_RAYLEIGH = 1, CH_LOS = 2, CH_TWOPATH = 3 };
+enum ChanKind : int { CH_RAYLEIGH = 1, CH_LOS = 2, CH_TWOPATH = 3, CH_TABLE = 4 };
 enum RxKind : int { RX_CNC = 1, RX_MCNC = 2 };
 
 constexpr int kMaxWaves = 16;
@@ -73,6 +73,7 @@ struct TrialParams {
   const double* f_over_c;        // [S]  f_k / c       (LoS / two-path phases)
   const double* tx_pos;          // [A*3]
   const double2* lut;            // [kLut64] fp64 ln / sincos tables (real.h; fp64 instances only)
+  const C* chan_tab;             // CH_TABLE: fixed in-band channel [A][S] (sub-carrier order k)
   int n_ant, n_sc, qam_l, half_bits;
   uint32_t label_mask;
   int pa_kind, cnc_pa_kind;
@@ -488,6 +489,15 @@ struct Channel {
           h[s] = cscale(h[s], v ? p.f_rel[k] : R(0));
         }
       }
+    } else if constexpr (CH == CH_TABLE) {
+      // the caller's fixed channel (Link.simulate reroll_chan=False): coalesced loads of the
+      // in-band row (f_rel is 1 for table engines: nothing is factored out)
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) {
+        bool v;
+        const int k = SL::k_of(s, t, S, v);
+        h[s] = v ? p.chan_tab[(size_t)a * S + k] : czero<R>();
+      }
     } else {
       const double tx = p.tx_pos[3 * a], ty = p.tx_pos[3 * a + 1], tz = p.tx_pos[3 * a + 2];
       const double dx = tx - rx[0], dy = ty - rx[1], dz = tz - rx[2];
@@ -584,7 +594,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 
   // RX position for LoS / two-path (mp_model.py:190-201; y uses rx_loc_x, a reference quirk)
   double rx[3] = {0.0, 0.0, 0.0};
-  if constexpr (CH != CH_RAYLEIGH) {
+  if constexpr (CH == CH_LOS || CH == CH_TWOPATH) {
     const uint4 w = philox4x32_10(make_uint4(0u, trial, ST_LOC, 0u), key);
     const double u0 = (double)w.x * 2.3283064365386963e-10, u1 = (double)w.y * 2.3283064365386963e-10;
     rx[0] = p.rx_x0 - p.rx_var * 0.5 + p.rx_var * u0;

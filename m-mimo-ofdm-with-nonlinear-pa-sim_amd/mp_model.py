@@ -190,25 +190,28 @@ class Link:
         return "los"
 
     def engine(self, reroll_chan: bool = True):
-        """The configured GPU engine for the current grid point (created lazily, per process)."""
+        """The configured GPU engine for the current grid point (created lazily, per process).
+
+        ``reroll_chan=False`` (mp_model.py:190-206: every trial sees the channel object's
+        current matrix) runs the table-channel instances on ``channel_mat_fd``."""
         kind = self._chan_kind()
-        if kind == "rayleigh" and not reroll_chan:
-            raise NotImplementedError("a fixed Rayleigh realisation (reroll_chan=False) is not supported: "
-                                      "the engine draws every trial's channel on the device")
+        table = None
+        if not reroll_chan:
+            table = np.asarray(self.my_miso_chan.channel_mat_fd, dtype=np.complex128)
+            kind = "table"
         dev = self.device if self.device is not None else _default_device()
         acquire_device_slot(dev)  # best effort here; simulate() waits for a slot
-        key = (dev, kind, bool(reroll_chan), self.is_mcnc, self.precision)
+        key = (dev, kind, bool(reroll_chan), self.is_mcnc, self.precision,
+               None if table is None else hash(table.tobytes()))
         if self._engine is None or self._engine_key != key:
             m = self.my_mod
             rx = self.my_standard_rx
-            if kind != "rayleigh" and self.rx_loc_y != self.rx_loc_x and not reroll_chan:
-                raise NotImplementedError("fixed LoS RX requires cord_y == cord_x")
             self._engine = _engine.Engine(
                 self.n_ant_val, m.n_sub_carr, m.n_fft, m.constel_size, m.cp_len, kind,
                 "mcnc" if self.is_mcnc else "cnc", self.my_array.positions(),
                 (self.rx_loc_x, self.rx_loc_y, rx.cord_z), self.rx_loc_var,
                 channel.carrier_freqs(m.n_fft, rx.carrier_spacing, rx.center_freq), reroll=reroll_chan, device=dev,
-                precision=self.precision)
+                precision=self.precision, chan_table=table)
             self._engine_key = key
         self._push_point()
         return self._engine

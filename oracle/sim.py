@@ -36,7 +36,7 @@ class SimConfig:
     p_hardness: float = 3.0
     ibo_db: float = 3.0
     snr_db: float = 20.0           # value passed to Link.set_snr (already Eb/N0 -> SNR)
-    channel: str = "rayleigh"      # rayleigh | los | two_path
+    channel: str = "rayleigh"      # rayleigh | los | two_path | table (fixed matrix table_h)
     receiver: str = "cnc"          # cnc | mcnc
     csi_eps: float | None = None
     center_freq: float = 3.5e9
@@ -47,6 +47,7 @@ class SimConfig:
     rx_loc_var: float = 10.0
     reroll: bool = True
     tx_pos: np.ndarray | None = field(default=None, repr=False)
+    table_h: np.ndarray | None = field(default=None, repr=False)  # [A, F] channel_mat_fd for "table"
 
     def __post_init__(self):
         if self.tx_pos is None:
@@ -60,6 +61,9 @@ def _const(cfg):
 def channel_inband(cfg: SimConfig, z_chan, loc_u):
     """True in-band channel [A, S] for one trial."""
     bins = rm.inband_bins(cfg.n_fft, cfg.n_sc)
+    if cfg.channel == "table":
+        # Link.simulate(reroll_chan=False): the channel object's matrix for every trial
+        return np.asarray(cfg.table_h, dtype=np.complex128)[:, bins]
     if cfg.channel == "rayleigh":
         # MisoRayleighFd.reroll_channel_coeffs (channel.py:262-275): CN(0,1) x FSPL at the
         # nominal RX position (the Rayleigh RX does not move, mp_model.py:191).

@@ -101,3 +101,42 @@ def test_edge_cases_empty_subsets_and_index_limits(prec):
     e, b, per = eng.run(3, top, 16, [0], False, per_trial=True)
     ref = sim.run_trials(cfg, 3, np.arange(top, top + 16), iters=[0])
     assert_counts_equal(per, ref, f"top trials {prec}")
+
+
+@pytest.mark.parametrize("prec", PRECISIONS)
+@pytest.mark.parametrize("receiver,csi", [("cnc", None), ("mcnc", None), ("cnc", 0.2)])
+def test_table_channel_vs_oracle(receiver, csi, prec):
+    """MIMO_CH_TABLE (Link.simulate(reroll_chan=False), mp_model.py:190-206): one fixed
+    channel matrix for every trial -- exact per-trial counts vs the oracle's fixed-matrix
+    path (parity with the reference unpinned: no fixture captures reroll_chan=False)."""
+    rng = np.random.default_rng(77)
+    A, S, F = 8, 256, 512
+    h = (rng.standard_normal((A, F)) + 1j * rng.standard_normal((A, F))) * np.sqrt(0.5) * 3e-7
+    cfg = sim.SimConfig(A, S, F, 16, ibo_db=1.0, snr_db=14.0, channel="table", receiver=receiver, csi_eps=csi,
+                        table_h=h)
+    iters = [0, 1, 2]
+    ref = sim.run_trials(cfg, 19, np.arange(48), iters=iters, incl_clean=True)
+    eng = engine_for(cfg, precision=prec)
+    _, _, per = eng.run(19, 0, 48, iters, True, per_trial=True)
+    print("table", receiver, csi, eng.describe(), per.sum(0), ref.sum(0))
+    assert "ch=4" in eng.describe()
+    assert_counts_equal(per, ref, f"table {receiver} {csi} {prec}")
+
+
+def test_link_fixed_rayleigh_channel_equals_table_engine():
+    """Link.simulate(reroll_chan=False) on a Rayleigh channel object runs every trial on the
+    object's channel_mat_fd (drawn from its seeded generator at construction, channel.py:209-212)."""
+    import ctypes
+    import multiprocessing as mp
+    from link_util import build_link
+    from mp_model import _seed64
+    link, _ = build_link(n_ant=8, n_sc=256, n_fft=512, M=16, ibo=1.0, bits_sent_max=1024 * 200,
+                         n_err_min=10 ** 12, device=0)
+    link.set_snr(14.0)
+    err, bits = mp.Array(ctypes.c_double, 3), mp.Array(ctypes.c_double, 3)
+    link.simulate(True, False, np.array([0, 1]), [4, 5, 6], err, bits)
+    cfg = sim.SimConfig(8, 256, 512, 16, ibo_db=1.0, snr_db=14.0, channel="table",
+                        table_h=link.my_miso_chan.channel_mat_fd)
+    ref = sim.run_trials(cfg, _seed64([4, 5, 6]), np.arange(200), iters=[0, 1], incl_clean=True)
+    np.testing.assert_array_equal(np.asarray(err[:], np.int64), ref.sum(0))
+    assert list(bits[:]) == [1024.0 * 200] * 3

@@ -122,12 +122,41 @@ def test_link_pickles_without_engine():
 
 
 def test_unsupported_channels_raise():
+    """QuaDRiGa / random-paths channel objects are rejected at Link construction."""
+    import copy
     import mp_model
+
+    class MisoQuadrigaFd:
+        channel_mat_fd = None
+
+    link, mod = build_link()
     with pytest.raises(NotImplementedError):
-        link, _ = build_link()
-        link._chan_kind = lambda: "rayleigh"
-        link.device = 0
-        link.engine(reroll_chan=False)
+        mp_model.Link(mod_obj=mod, array_obj=link.my_array, std_rx_obj=link.my_standard_rx,
+                      chan_obj=MisoQuadrigaFd(), noise_obj=copy.deepcopy(link.my_noise), rx_loc_var=10.0,
+                      n_err_min=10, bits_sent_max=100)
+
+
+@pytest.mark.parametrize("chan", ["rayleigh", "los", "two_path"])
+def test_fixed_channel_uses_the_channel_objects_matrix(monkeypatch, chan):
+    """simulate(reroll_chan=False) (mp_model.py:190-206): every trial sees the channel
+    object's current matrix -> a table-channel engine built from channel_mat_fd."""
+    import _engine
+    seen = {}
+
+    class Capture:
+        def __init__(self, *a, **k):
+            seen["args"], seen["kw"] = a, k
+
+        def set_point(self, *a, **k):
+            pass
+
+    monkeypatch.setattr(_engine, "Engine", Capture)
+    link, _ = build_link(chan=chan, device=0)
+    link.engine(reroll_chan=False)
+    assert seen["args"][5] == "table"
+    np.testing.assert_array_equal(seen["kw"]["chan_table"], link.my_miso_chan.channel_mat_fd)
+    link.engine(reroll_chan=True)
+    assert seen["args"][5] == chan and seen["kw"]["chan_table"] is None
 
 
 def _slot_child(dev, q):
