@@ -508,7 +508,12 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
   e->desc = buf;
 
   // segments (point, first trial, count) packed into launches of <= kChunk blocks
-  constexpr uint64_t kChunk = 1ull << 20;
+  // Trials per launch: 2^20 (MIMO_MAX_LAUNCH_TRIALS lowers it, for tests of the splitting).
+  uint64_t kChunk = 1ull << 20;
+  if (const char* env = std::getenv("MIMO_MAX_LAUNCH_TRIALS")) {
+    const uint64_t v = std::strtoull(env, nullptr, 10);
+    if (v >= 1 && v < kChunk) kChunk = v;
+  }
   struct Seg {
     int point;
     uint64_t first, n;
@@ -530,10 +535,10 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
   }
   size_t max_seg = 0;
   for (auto& l : launches) max_seg = std::max(max_seg, l.size());
-  if (int rc = ensure_cap(e->d_counts, e->counts_cap, (size_t)kChunk * n_idx)) return rc;
+  if (int rc = ensure_cap(e->d_counts, e->counts_cap, (size_t)(1ull << 20) * n_idx)) return rc;
   if (int rc = ensure_cap(e->d_tot, e->tot_cap, (size_t)n_points * n_idx)) return rc;
   if (int rc = ensure_cap(e->d_start, e->start_cap, max_seg + 1)) return rc;
-  const size_t max_slices = max_seg + kChunk / kSlice + 1;
+  const size_t max_slices = max_seg + (size_t)(kChunk / kSlice) + 1;
   if (int rc = ensure_cap(e->d_slice_first, e->slice_cap, max_slices + 1)) return rc;
   if (int rc = ensure_cap(e->d_point_of, e->point_of_cap, max_slices)) return rc;
   HIP_TRY(hipMemsetAsync(e->d_tot, 0, sizeof(unsigned long long) * n_points * n_idx, e->stream));

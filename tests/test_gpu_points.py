@@ -91,3 +91,20 @@ def test_gloo_sharded_sweep_through_real_link_equals_single_process(tmp_path):
         got = np.load(os.path.join(tmp_path, "r%d.npy" % r))
         np.testing.assert_array_equal(got[0], ref_err)
         np.testing.assert_array_equal(got[1], ref_bits)
+
+
+def test_launch_splitting_keeps_every_trial(monkeypatch):
+    """Points larger than one launch and launches holding several points
+    (MIMO_MAX_LAUNCH_TRIALS=50: the 2^20-trial limit scaled down): per-trial counts in
+    point order and per-point totals equal one launch per point."""
+    cfg = sim.SimConfig(8, 256, 512, 16, ibo_db=1.0, snr_db=12.0)
+    eng = engine_for(cfg)
+    pts = [_point_of(sim.SimConfig(8, 256, 512, 16, ibo_db=i, snr_db=s)) for i, s in [(1.0, 12.0), (2.0, 9.0),
+                                                                                        (0.5, 15.0)]]
+    ns, firsts, seeds = [120, 7, 61], [0, 500, 33], [8, 9, 10]
+    ref_err, _, ref_per = eng.run_points(pts, seeds, firsts, ns, [0, 2], True, per_trial=True)
+    monkeypatch.setenv("MIMO_MAX_LAUNCH_TRIALS", "50")
+    err, bits, per = eng.run_points(pts, seeds, firsts, ns, [0, 2], True, per_trial=True)
+    np.testing.assert_array_equal(per, ref_per)
+    np.testing.assert_array_equal(err, ref_err)
+    assert np.all(bits[:, 0] == np.asarray(ns) * 256 * 4)
