@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/mimo_engine.h"
@@ -62,8 +63,14 @@ double alpha_exact(double g2) {
 // at 64 nodes, converted to monomials in x for a Horner evaluation in fp32.  Max relative
 // error ~1e-7 for IBO in [-10, 30] dB (fp32 rounding level); the kernel falls back to
 // the exact formula outside the interval.
-template <typename P>
-void fit_alpha(double g0sq, P& p) {
+struct AlphaFit {
+  double apoly[9];   // fp32 Horner monomials in x
+  double xlim;
+  double acheb[19];  // fp64 Clenshaw coefficients in t = x / xlim
+};
+
+AlphaFit fit_alpha(double g0sq) {
+  AlphaFit p{};
   constexpr int N = 64, D = 8;
   constexpr double L = 0.25;
   double c[D + 1] = {0};
@@ -88,9 +95,8 @@ void fit_alpha(double g0sq, P& p) {
     }
   }
   double sc = 1.0;
-  using R = std::remove_reference_t<decltype(p.apoly[0])>;
-  for (int i = 0; i <= D; ++i, sc /= L) p.apoly[i] = (R)(mono[i] * sc);
-  p.alpha_xlim = (R)L;
+  for (int i = 0; i <= D; ++i, sc /= L) p.apoly[i] = mono[i] * sc;
+  p.xlim = L;
   // fp64: Chebyshev coefficients of degree 18 on the same interval (Clenshaw in the kernel),
   // at 64 nodes in long double
   constexpr int D64 = 18;
@@ -106,6 +112,7 @@ void fit_alpha(double g0sq, P& p) {
     }
     p.acheb[k] = (double)(ck * (k == 0 ? 1.0L : 2.0L) / N);
   }
+  return p;
 }
 
 // fp64 Box-Muller tables (real.h ln_lut / sincos_lut), computed in long double.
@@ -167,14 +174,17 @@ struct mimo_engine {
   size_t counts_cap = 0;
   unsigned long long* d_tot = nullptr;    // [points][n_idx] totals of one run
   size_t tot_cap = 0;
-  void* d_points = nullptr;                // TrialParams<R>[segments of one launch]
-  size_t points_cap = 0;                   // bytes
-  uint32_t* d_start = nullptr;             // [segments + 1] block offsets
-  uint32_t* d_slice_first = nullptr;       // [slices + 1] reduction slices (<= kSlice trials, one point each)
-  int32_t* d_point_of = nullptr;           // [slices] point index
-  size_t start_cap = 0, slice_cap = 0, point_of_cap = 0;
+  // per-launch tables in one device blob, filled by one copy from a pinned host buffer:
+  // TrialParams<R>[segments] | uint32 block offsets [segments + 1] |
+  // uint32 reduction-slice starts [slices + 1] (<= kSlice trials, one point each) | int32 point of slice [slices]
+  char* d_blob = nullptr;
+  char* h_blob = nullptr;
+  size_t blob_cap = 0, hblob_cap = 0;
   double d0 = 1.0;
   double last_ms = 0.0;
+  // fit_alpha results per IBO (bit pattern of 10^(IBO/10)): the long-double fit costs
+  // ~0.3 ms, paid once per IBO instead of once per point and batch of a sweep
+  std::unordered_map<uint64_t, AlphaFit> alpha_fits;
   std::string desc;
 };
 
@@ -285,7 +295,7 @@ int validate_point(const mimo_engine* e, const mimo_point* pt) {
 
 // Per-point fields of the kernel parameters (the reference's per-point object state).
 template <typename R>
-void fill_point(const mimo_engine* e, const mimo_point& pt, uint64_t seed, uint64_t first_trial,
+void fill_point(mimo_engine* e, const mimo_point& pt, uint64_t seed, uint64_t first_trial,
                 mimo::TrialParams<R>& p) {
   const mimo_config& c = e->cfg;
   const bool csi = pt.csi_eps >= 0;
@@ -304,7 +314,20 @@ void fill_point(const mimo_engine* e, const mimo_point& pt, uint64_t seed, uint6
   p.toi_cnc = (R)pt.cnc_toi_coeff;
   p.inv_alpha_cnc = (R)(1.0 / pt.cnc_alpha);
   p.alpha_c = (R)(std::pow(10.0, pt.ibo_db / 10.0) * c.n_sub_carr / c.n_ant);
-  fit_alpha(std::pow(10.0, pt.ibo_db / 10.0), p);
+  {
+    const double g0sq = std::pow(10.0, pt.ibo_db / 10.0);
+    uint64_t key;
+    std::memcpy(&key, &g0sq, sizeof key);
+    auto it = e->alpha_fits.find(key);
+    if (it == e->alpha_fits.end()) {
+      if (e->alpha_fits.size() >= 4096) e->alpha_fits.clear();
+      it = e->alpha_fits.emplace(key, fit_alpha(g0sq)).first;
+    }
+    const AlphaFit& af = it->second;
+    for (int i = 0; i < 9; ++i) p.apoly[i] = (R)af.apoly[i];
+    p.alpha_xlim = (R)af.xlim;
+    for (int k = 0; k < 19; ++k) p.acheb[k] = af.acheb[k];
+  }
   p.es_over_snr = (R)(pt.avg_symbol_power / std::pow(10.0, pt.snr_db / 10.0));
   p.csi_a = csi ? (R)std::sqrt(1.0 - pt.csi_eps * pt.csi_eps) : R(1);
   p.csi_b = csi ? (R)pt.csi_eps : R(0);
@@ -537,10 +560,7 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
   for (auto& l : launches) max_seg = std::max(max_seg, l.size());
   if (int rc = ensure_cap(e->d_counts, e->counts_cap, (size_t)(1ull << 20) * n_idx)) return rc;
   if (int rc = ensure_cap(e->d_tot, e->tot_cap, (size_t)n_points * n_idx)) return rc;
-  if (int rc = ensure_cap(e->d_start, e->start_cap, max_seg + 1)) return rc;
   const size_t max_slices = max_seg + (size_t)(kChunk / kSlice) + 1;
-  if (int rc = ensure_cap(e->d_slice_first, e->slice_cap, max_slices + 1)) return rc;
-  if (int rc = ensure_cap(e->d_point_of, e->point_of_cap, max_slices)) return rc;
   HIP_TRY(hipMemsetAsync(e->d_tot, 0, sizeof(unsigned long long) * n_points * n_idx, e->stream));
   double ms_total = 0.0;
   uint64_t rows_done = 0;
@@ -589,50 +609,53 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
     // per-point parameter table (host), built once
     std::vector<TP> ptab(n_points, base);
     for (int i = 0; i < n_points; ++i) fill_point(e, pts[i], seeds[i], 0, ptab[i]);
-    char* dp = static_cast<char*>(e->d_points);
-    if (int rc = ensure_cap(dp, e->points_cap, max_seg * sizeof(TP))) return rc;
-    e->d_points = dp;
-    std::vector<TP> seg_tab;
-    std::vector<uint32_t> start;
-    std::vector<int32_t> point_of;
+    auto up16 = [](size_t b) { return (b + 15) & ~size_t(15); };
+    const size_t o_start = up16(max_seg * sizeof(TP)), o_slice = o_start + up16((max_seg + 1) * sizeof(uint32_t)),
+                 o_pof = o_slice + up16((max_slices + 1) * sizeof(uint32_t)),
+                 blob = o_pof + up16(max_slices * sizeof(int32_t));
+    if (int rc = ensure_cap(e->d_blob, e->blob_cap, blob)) return rc;
+    if (blob > e->hblob_cap) {
+      if (e->h_blob) HIP_TRY(hipHostFree(e->h_blob));
+      e->h_blob = nullptr;
+      HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&e->h_blob), blob, hipHostMallocDefault));
+      e->hblob_cap = blob;
+    }
+    TP* seg_tab = reinterpret_cast<TP*>(e->h_blob);
+    uint32_t* start = reinterpret_cast<uint32_t*>(e->h_blob + o_start);
+    uint32_t* slice_first = reinterpret_cast<uint32_t*>(e->h_blob + o_slice);
+    int32_t* point_of = reinterpret_cast<int32_t*>(e->h_blob + o_pof);
     for (auto& l : launches) {
-      seg_tab.clear();
-      start.assign(1, 0u);
-      point_of.clear();
-      std::vector<uint32_t> slice_first(1, 0u);
+      size_t nseg = 0, nsl = 0;
+      start[0] = 0u;
+      slice_first[0] = 0u;
       for (auto& sg : l) {
         TP q = ptab[sg.point];
         q.first_trial = sg.first;
-        seg_tab.push_back(q);
-        const uint32_t b0 = start.back();
-        start.push_back(b0 + (uint32_t)sg.n);
+        seg_tab[nseg] = q;
+        const uint32_t b0 = start[nseg];
+        start[++nseg] = b0 + (uint32_t)sg.n;
         for (uint32_t o = 0; o < (uint32_t)sg.n; o += kSlice) {
-          slice_first.push_back(b0 + std::min<uint32_t>((uint32_t)sg.n, o + kSlice));
-          point_of.push_back(sg.point);
+          slice_first[++nsl] = b0 + std::min<uint32_t>((uint32_t)sg.n, o + kSlice);
+          point_of[nsl - 1] = sg.point;
         }
       }
-      const uint32_t nb = start.back();
+      const uint32_t nb = start[nseg];
       TP kp = base;
-      kp.points = reinterpret_cast<const TP*>(e->d_points);
-      kp.point_start = e->d_start;
-      kp.n_points = (int)l.size();
+      kp.points = reinterpret_cast<const TP*>(e->d_blob);
+      kp.point_start = reinterpret_cast<const uint32_t*>(e->d_blob + o_start);
+      kp.n_points = (int)nseg;
       kp.seed = seg_tab[0].seed;  // unused by the kernel (read from the table)
-      HIP_TRY(hipMemcpyAsync(e->d_points, seg_tab.data(), seg_tab.size() * sizeof(TP), hipMemcpyHostToDevice,
-                             e->stream));
-      HIP_TRY(hipMemcpyAsync(e->d_start, start.data(), start.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                             e->stream));
-      HIP_TRY(hipMemcpyAsync(e->d_point_of, point_of.data(), point_of.size() * sizeof(int32_t),
-                             hipMemcpyHostToDevice, e->stream));
-      HIP_TRY(hipMemcpyAsync(e->d_slice_first, slice_first.data(), slice_first.size() * sizeof(uint32_t),
-                             hipMemcpyHostToDevice, e->stream));
+      // the whole blob (unused tails included: one contiguous DMA)
+      HIP_TRY(hipMemcpyAsync(e->d_blob, e->h_blob, o_pof + nsl * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
       HIP_TRY(hipEventRecord(e->ev0, e->stream));
       bool found = false;
       hipError_t le = launch(key, dim3(nb), e->stream, kp, &found);
       if (!found) return fail(MIMO_ENOKERNEL, std::string("no kernel instance for ") + buf);
       if (le != hipSuccess) return fail(MIMO_EHIP, std::string("trial kernel launch: ") + hipGetErrorString(le));
       HIP_TRY(hipEventRecord(e->ev1, e->stream));
-      hipLaunchKernelGGL(reduce_counts, dim3((unsigned)point_of.size(), n_idx), dim3(256), 0, e->stream,
-                         e->d_counts, e->d_slice_first, e->d_point_of, n_idx, e->d_tot);
+      hipLaunchKernelGGL(reduce_counts, dim3((unsigned)nsl, n_idx), dim3(256), 0, e->stream, e->d_counts,
+                         reinterpret_cast<const uint32_t*>(e->d_blob + o_slice),
+                         reinterpret_cast<const int32_t*>(e->d_blob + o_pof), n_idx, e->d_tot);
       HIP_TRY(hipGetLastError());
       if (per_trial)
         HIP_TRY(hipMemcpyAsync(per_trial + rows_done * n_idx, e->d_counts, (size_t)nb * n_idx * sizeof(uint32_t),
@@ -718,10 +741,8 @@ void mimo_engine_destroy(mimo_engine* e) {
     (void)hipFree(e->d_tx_pos);
     if (e->d_tot) (void)hipFree(e->d_tot);
     if (e->d_counts) (void)hipFree(e->d_counts);
-    if (e->d_points) (void)hipFree(e->d_points);
-    if (e->d_start) (void)hipFree(e->d_start);
-    if (e->d_point_of) (void)hipFree(e->d_point_of);
-    if (e->d_slice_first) (void)hipFree(e->d_slice_first);
+    if (e->d_blob) (void)hipFree(e->d_blob);
+    if (e->h_blob) (void)hipHostFree(e->h_blob);
     (void)hipEventDestroy(e->ev0);
     (void)hipEventDestroy(e->ev1);
     (void)hipStreamDestroy(e->stream);
