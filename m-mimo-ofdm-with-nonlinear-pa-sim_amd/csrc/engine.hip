@@ -161,6 +161,8 @@ struct mimo_engine {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float2* d_tw[2] = {nullptr, nullptr};  // fp32 stage twiddles for team_size(F), alt_team_size(F)
   double2* d_tw64 = nullptr;              // fp64 stage twiddles for team_size64(F)
+  double2* d_twave64 = nullptr;           // wave-split FFT twiddles (wave_fft.h) where the instance uses it
+  float2* d_twave32 = nullptr;
   double2* d_lut64 = nullptr;             // fp64 Box-Muller tables (lut64_table)
   float2* d_tab32 = nullptr;              // MIMO_CH_TABLE channel, fp32 / fp64 copies
   double2* d_tab64 = nullptr;
@@ -353,7 +355,7 @@ int ensure_device(mimo_engine* e) {
   const int F = e->cfg.n_fft, S = e->cfg.n_sub_carr, A = e->cfg.n_ant;
   // team-FFT stage twiddles per team size (team_fft.h plan), computed in double:
   // stage s, entry [r][jm] = exp(-j 2 pi e / F) with e = jm r F / (NS R)
-  auto twiddles = [F](int T, auto cvt) {
+  auto twiddles_of = [](int F, int T, auto cvt) {
     const int P = F / T;
     using V = decltype(cvt(0.0, 0.0));
     std::vector<V> tw(std::max(1, mimo::fft_tw_total(F, P)), cvt(0.0, 0.0));
@@ -369,10 +371,25 @@ int ensure_device(mimo_engine* e) {
     }
     return tw;
   };
+  auto twiddles = [&](int T, auto cvt) { return twiddles_of(F, T, cvt); };
   auto to_f32 = [](double c, double s) { return make_float2((float)c, (float)s); };
   auto to_f64 = [](double c, double s) { return make_double2(c, s); };
   std::vector<float2> tws[2] = {twiddles(mimo::team_size(F), to_f32), twiddles(mimo::alt_team_size(F), to_f32)};
   std::vector<double2> tw64 = twiddles(mimo::team_size64(F), to_f64);
+  // wave-split FFT (wave_fft.h): the one-wave sub-transform's stages, then exp(-j 2 pi n / F)
+  auto wave_twiddles = [&](int T, auto cvt) {
+    auto tw = twiddles_of(mimo::wave_fft_fw(F, T), 64, cvt);
+    tw.resize(mimo::wave_fft_tw_inter(F, T));
+    for (int n = 0; n < F; ++n) {
+      const double ang = -2.0 * M_PI * (double)n / (double)F;
+      tw.push_back(cvt(std::cos(ang), std::sin(ang)));
+    }
+    return tw;
+  };
+  std::vector<double2> twave64;
+  std::vector<float2> twave32;
+  if (mimo::wave_fft_used(F, mimo::team_size64(F), true)) twave64 = wave_twiddles(mimo::team_size64(F), to_f64);
+  if (mimo::wave_fft_used(F, mimo::team_size(F), false)) twave32 = wave_twiddles(mimo::team_size(F), to_f32);
   // in-band sub-carrier k -> bin (modulation.py:266-267)
   std::vector<float> f_rel(S);
   std::vector<double> f_rel64(S), f_over_c(S);
@@ -420,6 +437,14 @@ int ensure_device(mimo_engine* e) {
   HIP_TRY(hipMemcpy(e->d_lut64, lut.data(), sizeof(double2) * lut.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&e->d_tw64, sizeof(double2) * tw64.size()));
   HIP_TRY(hipMemcpy(e->d_tw64, tw64.data(), sizeof(double2) * tw64.size(), hipMemcpyHostToDevice));
+  if (!twave64.empty()) {
+    HIP_TRY(hipMalloc(&e->d_twave64, sizeof(double2) * twave64.size()));
+    HIP_TRY(hipMemcpy(e->d_twave64, twave64.data(), sizeof(double2) * twave64.size(), hipMemcpyHostToDevice));
+  }
+  if (!twave32.empty()) {
+    HIP_TRY(hipMalloc(&e->d_twave32, sizeof(float2) * twave32.size()));
+    HIP_TRY(hipMemcpy(e->d_twave32, twave32.data(), sizeof(float2) * twave32.size(), hipMemcpyHostToDevice));
+  }
   HIP_TRY(hipMalloc(&e->d_f_rel64, sizeof(double) * S));
   HIP_TRY(hipMalloc(&e->d_ant_rel64, sizeof(double) * A));
   HIP_TRY(hipMemcpy(e->d_f_rel64, f_rel64.data(), sizeof(double) * S, hipMemcpyHostToDevice));
@@ -572,11 +597,13 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
     TP base{};
     if constexpr (F64) {
       base.tw = e->d_tw64;
+      base.tw_wave = e->d_twave64;
       base.ant_rel = e->d_ant_rel64;
       base.f_rel = e->d_f_rel64;
       base.chan_tab = e->d_tab64;
     } else {
       base.tw = e->d_tw[key.T == mimo::team_size(c.n_fft) ? 0 : 1];
+      base.tw_wave = key.T == mimo::team_size(c.n_fft) ? e->d_twave32 : nullptr;
       base.ant_rel = e->d_ant_rel;
       base.f_rel = e->d_f_rel;
       base.chan_tab = e->d_tab32;
@@ -731,6 +758,8 @@ void mimo_engine_destroy(mimo_engine* e) {
     (void)hipFree(e->d_tw[1]);
     (void)hipFree(e->d_f_rel);
     (void)hipFree(e->d_tw64);
+    if (e->d_twave64) (void)hipFree(e->d_twave64);
+    if (e->d_twave32) (void)hipFree(e->d_twave32);
     (void)hipFree(e->d_lut64);
     if (e->d_tab32) (void)hipFree(e->d_tab32);
     if (e->d_tab64) (void)hipFree(e->d_tab64);

@@ -224,8 +224,22 @@ struct Dft {
   };
 };
 
+// Exchange synchronisation: the whole team (s_barrier) or, for a one-wave transform
+// (WAVE, wave_fft.h), the wave alone.  A wave's LDS instructions execute in issue order,
+// so its own exchanges need only a compiler-level fence, no hardware barrier.
+template <bool WAVE>
+__device__ __forceinline__ void xchg_sync() {
+  if constexpr (WAVE) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- team FFT
-template <int F, int T, int NBUF = 2, typename Re = float>
+template <int F, int T, int NBUF = 2, typename Re = float, bool WAVE = false>
 struct TeamFft {
   using C = cx<Re>;
   static constexpr int P = F / T;
@@ -244,6 +258,7 @@ struct TeamFft {
   static constexpr int psh(int S) { return S == 0 ? PAD0 : MIMO_PADN_SHIFT; }
   static constexpr int LDS_ELEMS = F + F / (1 << (PAD0 < MIMO_PADN_SHIFT ? PAD0 : MIMO_PADN_SHIFT));
   static_assert((1 << LOG_F) == F && (1 << LOG_P) == P && P >= 2, "power-of-two sizes");
+  static_assert(!WAVE || T == 64, "wave-local transforms are one wave");
 
   static constexpr int bits(int s) { return fft_bits(F, P, s); }
   static constexpr int bits_before(int s) { return fft_bits_before(F, P, s); }
@@ -316,7 +331,7 @@ struct TeamFft {
       // One buffer: everyone must have read the previous exchange before it is
       // overwritten.  The barrier sits after this stage's twiddle loads and DFT, so
       // their latency overlaps the previous exchange's reads.
-      if constexpr (NBUF == 1 && I == 0 && !MIMO_DIAG_NOPREBAR) __syncthreads();
+      if constexpr (NBUF == 1 && I == 0 && !MIMO_DIAG_NOPREBAR) xchg_sync<WAVE>();
       // pad(base + r NS) == pad(base) + pad(r NS) for power-of-two NS, R, T (the
       // padding never splits a write group): one address per i, immediate offsets.
       C* wb = buf + pad<S>((j / NS) * NS * R + jm);
@@ -424,7 +439,7 @@ struct TeamFft {
     butterflies<S, DIR, ZM>(d, buf, w0, t, no_xchg);
     if constexpr (!LAST) {
       if (!no_xchg) {
-        __syncthreads();
+        xchg_sync<WAVE>();
         const C* rb = buf + pad<S>(t);
 #pragma unroll
         for (int m = 0; m < P; ++m) d[m] = rb[pad<S>(T * m)];

@@ -28,8 +28,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "philox.h"
 #include "team_fft.h"
+#include "wave_fft.h"
 
 namespace mimo {
 
@@ -68,6 +71,7 @@ struct TrialParams {
   uint64_t first_trial;
   uint32_t* counts;              // [n_trials][n_idx]
   const C* tw;                   // team-FFT stage twiddles of (F, T) (team_fft.h fft_tw_off)
+  const C* tw_wave;              // wave-split FFT twiddles of (F, T) (wave_fft.h), or null
   const R* ant_rel;              // [A]  d0 / d_a      (Rayleigh FSPL, relative)
   const R* f_rel;                // [S]  fc / f_k      (f_k float32-quantised as in the reference)
   const double* f_over_c;        // [S]  f_k / c       (LoS / two-path phases)
@@ -562,7 +566,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   }
   using CParams = const __attribute__((address_space(4))) TrialParams<R>;
   CParams& p = *(CParams*)(p0.points + pi);
-  using FFT = TeamFft<F, T, NBUF, R>;
+  constexpr bool WAVEFFT = wave_fft_used(F, T, sizeof(R) == 8);
+  using FFT = std::conditional_t<WAVEFFT, WaveFft<F, T, R>, TeamFft<F, T, NBUF, R>>;
   using SL = Slots<F, T, NSLOT, ALIGNED>;
   using CHN = Channel<R, F, T, NSLOT, ALIGNED, CH>;
   constexpr int P = FFT::P;
@@ -779,9 +784,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       }
       SL::scatter(d, x, t0);
       if (!MIMO_ABL(p, ABL_FFT))
-        FFT::template run<+1, 0, SL::zero_mask()>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_ifft);
+        FFT::template run<+1, 0, SL::zero_mask()>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_ifft);
       if (!MIMO_ABL(p, ABL_PA)) pa_block(p.pa_kind, d, p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
-      if (!MIMO_ABL(p, ABL_FFT)) FFT::template run_second<-1>(d, lds, p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_fft);
+      if (!MIMO_ABL(p, ABL_FFT)) FFT::template run_second<-1>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_fft);
       if constexpr (PIPE) {
         if (MIMO_ABL(p, ABL_FFT)) {  // no transforms ran, so no exchange windows (ABL_XCHG keeps them)
 #pragma unroll
@@ -919,9 +924,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       for (int s = 0; s < NSLOT; ++s)
         x[s] = ((valid_mask >> s) & 1u) ? cscale(qam_point<R>(lh[s], L, hb), inv_sqrt_f) : czero<R>();
       SL::scatter(d, x, t0);
-      FFT::template run<+1, 0, SL::zero_mask()>(d, lds, p.tw, t);
+      FFT::template run<+1, 0, SL::zero_mask()>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t);
       pa_block(p.cnc_pa_kind, d, p.sat_cnc, p.sqrt_sat_cnc, p.inv_sat_cnc, p.rapp_p, p.toi_cnc);
-      FFT::template run_second<-1>(d, lds, p.tw, t);
+      FFT::template run_second<-1>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t);
       const R sc = inv_sqrt_f * p.inv_alpha_cnc;
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
