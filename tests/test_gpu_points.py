@@ -108,3 +108,34 @@ def test_launch_splitting_keeps_every_trial(monkeypatch):
     np.testing.assert_array_equal(per, ref_per)
     np.testing.assert_array_equal(err, ref_err)
     assert np.all(bits[:, 0] == np.asarray(ns) * 256 * 4)
+
+
+def test_many_small_points_one_launch_and_growing_tables():
+    """Thousands of 1-3-trial points (the pinned per-launch tables grow past their first
+    size and across the 4096-trial reduction slices), then a small call on the same
+    engine: per-point totals equal the per-trial counts, and every trial's counts equal
+    a launch of that point alone."""
+    cfg = sim.SimConfig(8, 256, 512, 16, ibo_db=1.0, snr_db=12.0)
+    eng = engine_for(cfg)
+    rng = np.random.default_rng(7)
+    base = [_point_of(sim.SimConfig(8, 256, 512, 16, ibo_db=float(i), snr_db=float(s)))
+            for i, s in [(0.0, 8.0), (1.0, 12.0), (3.0, 16.0), (6.0, 10.0)]]
+    small_err, _, small_per = eng.run_points(base[:2], [1, 2], [0, 0], [3, 2], [0, 1], False, per_trial=True)
+    n = 3000
+    kinds = rng.integers(0, len(base), n)
+    pts = [base[k] for k in kinds]
+    ns = rng.integers(1, 4, n)
+    seeds = [int(x) for x in rng.integers(1, 1 << 40, n)]
+    firsts = [int(x) for x in rng.integers(0, 1 << 20, n)]
+    err, bits, per = eng.run_points(pts, seeds, firsts, [int(x) for x in ns], [0, 1], False, per_trial=True)
+    assert per.shape == (int(ns.sum()), 2)
+    got = np.split(per, np.cumsum(ns)[:-1])
+    for i in range(n):
+        np.testing.assert_array_equal(err[i], got[i].sum(0))
+        assert np.all(bits[i] == ns[i] * 256 * 4)
+    for i in rng.choice(n, 12, replace=False):  # spot checks against one-point launches
+        _, _, ref = eng.run_points([pts[i]], [seeds[i]], [firsts[i]], [int(ns[i])], [0, 1], False, per_trial=True)
+        np.testing.assert_array_equal(got[i], ref)
+    err2, _, per2 = eng.run_points(base[:2], [1, 2], [0, 0], [3, 2], [0, 1], False, per_trial=True)
+    np.testing.assert_array_equal(per2, small_per)
+    np.testing.assert_array_equal(err2, small_err)
