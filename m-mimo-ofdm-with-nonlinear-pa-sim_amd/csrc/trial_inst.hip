@@ -50,7 +50,7 @@ struct Profile {
 };
 constexpr Profile profile_for(int T, bool aligned, int ch) {
   const int P = kF / T;
-  if (kF64 && kF >= 8192) return Profile{2, 1, false};  // 136 KiB exchange buffer: one team per CU
+  if (kF64 && kF >= 8192) return Profile{2, 1, false};  // 136 KiB exchange buffer: one team per CU (T = 1024: 4 waves/SIMD)
   if (kF64) return Profile{MIMO_F64_MINW, MIMO_F64_NBUF, MIMO_F64_SYMW != 0};
   if (!aligned) return Profile{2, kF >= 4096 ? 1 : 2, true};  // one buffer from F = 4096: 2 teams/CU
   if (ch == CH_TWOPATH && MIMO_TWOPATH_W2) return Profile{2, 2, false};  // fp64 geometry: register-heavy

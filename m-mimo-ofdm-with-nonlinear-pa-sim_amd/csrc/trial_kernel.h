@@ -58,7 +58,7 @@ constexpr int kMaxCsiAnt = 512;  // CSI-error runs: antennas (LDS per team; engi
 #define MIMO_HPIPE 1  // draw antenna a+1's channel inside antenna a's FFT exchanges (aligned Rayleigh)
 #endif
 #ifndef MIMO_HPIPE64_OFF_F
-#define MIMO_HPIPE64_OFF_F 2048  // fp64: no channel pipeline up to this FFT size (A/B knob)
+#define MIMO_HPIPE64_OFF_F 8192  // fp64: no channel pipeline up to this FFT size (A/B knob; F 4096: -2.3 %, F 8192: -20 %)
 #endif
 #ifndef MIMO_VK_DPP
 #define MIMO_VK_DPP 1  // per-antenna precoding-power wave sum by DPP (0: __shfl_xor)
@@ -711,8 +711,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     for (int s = 0; s < NSLOT; ++s) acc[s] = czero<R>();
     // Software pipeline (PIPE): antenna a+1's channel draws (one Philox call per chunk)
     // run inside antenna a's FFT exchanges, where the wave otherwise waits on LDS.
-    // fp64 at F <= 2048: off (the pipelined draws' registers cost more than the exchange
-    // windows hide: -1.8 % without, profiles/r02/ab/ab64_2048.json).
+    // fp64 at F <= 4096: off (the pipelined draws' registers cost more than the exchange
+    // windows hide: -1.8 % without at F 2048, profiles/r02/ab/ab64_2048.json; -2.3 % at
+    // F 4096 with the wave-split FFT, scratch 140 -> 36 B/lane, profiles/r02/ab/ab4k_pipe_off.json).
     constexpr bool PIPE = MIMO_HPIPE && ALIGNED && CH == CH_RAYLEIGH && !CSI && !(sizeof(R) == 8 && F <= MIMO_HPIPE64_OFF_F);
     C hnext[PIPE ? NSLOT : 1];
     if constexpr (PIPE) {

@@ -10,13 +10,18 @@ namespace mimo {
 constexpr int team_size(int F) { return F >= 1024 ? F / 16 : 64; }
 // fp64 instances: 8 points per thread from F = 512 up (a complex double takes 4 VGPRs,
 // so P = 8 holds the same 32 data registers as the fp32 team's P = 16), one wave below.
-// F = 8192: 16 points per thread (a 1024-thread team would cap the waves at 128 VGPRs;
-// its one 136 KiB exchange buffer allows one team per CU either way).
+// F = 8192: 8 points per thread as well (T = 1024, 4 waves/SIMD at 128 VGPRs): its one
+// 136 KiB exchange buffer allows one team per CU either way, and the 16-point team
+// (T = 512, 2 waves/SIMD) measured 3.3 % slower despite fewer spills
+// (profiles/r02/ab/ab8k_f64_team_pipe.json).
 #ifndef MIMO_F64_P16_MAXF
 #define MIMO_F64_P16_MAXF 0  // A/B knob: fp64 instances with 16 points per thread up to this F
 #endif
+#ifndef MIMO_F64_T8192
+#define MIMO_F64_T8192 1024  // fp64 F >= 8192 team size (A/B knob; 1024: 8 points per thread, 4 waves/SIMD, -3.3 % vs 512)
+#endif
 constexpr int team_size64(int F) {
-  return F >= 8192 ? F / 16 : (F <= MIMO_F64_P16_MAXF && F >= 1024) ? F / 16 : F >= 512 ? F / 8 : 64;
+  return F >= 8192 ? F / (8192 / MIMO_F64_T8192) : (F <= MIMO_F64_P16_MAXF && F >= 1024) ? F / 16 : F >= 512 ? F / 8 : 64;
 }
 // Alternative team (8 points per thread: half the registers, 2x the waves, one more
 // LDS exchange per transform), selectable with MIMO_TEAM=<T> for A/B measurements.
