@@ -60,6 +60,12 @@ constexpr int kMaxCsiAnt = 512;  // CSI-error runs: antennas (LDS per team; engi
 #ifndef MIMO_HPIPE64_OFF_F
 #define MIMO_HPIPE64_OFF_F 8192  // fp64: no channel pipeline up to this FFT size (A/B knob; F 4096: -2.3 %, F 8192: -20 %)
 #endif
+#ifndef MIMO_REGDIET
+#define MIMO_REGDIET 3  // fp64 register diet: bit 0 symbols rebuilt per antenna, bit 1 |H|^2 recomputed
+#endif
+#ifndef MIMO_REGDIET_MINF
+#define MIMO_REGDIET_MINF 8192  // ... from this FFT size (F 8192: -2.1 %; F 2048 bit 1: +0.8 %, off)
+#endif
 #ifndef MIMO_VK_DPP
 #define MIMO_VK_DPP 1  // per-antenna precoding-power wave sum by DPP (0: __shfl_xor)
 #endif
@@ -695,16 +701,35 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // MAIN: symbols = tx labels, combine with the true channel, accumulate g (alpha_a).
   // MCNC: symbols = detected labels, combine with the estimated channel (corrector.py:198-200).
   // The symbols enter pre-weighted, symw = s / ||Hhat|| / sqrt(F) (0 on invalid slots).
-  C symw_r[SYMW_LDS ? 1 : NSLOT];
+  // SYMW_RE (register diet, MIMO_REGDIET bit 0, symbols not in LDS): keep the labels
+  // (1 VGPR per slot) and rebuild the symbol per antenna instead of holding it (4 VGPRs
+  // in fp64); the opaque copies stop the compiler from hoisting it back out of the loop.
+  constexpr bool SYMW_RE = !SYMW_LDS && (MIMO_REGDIET & 1) && sizeof(R) == 8 && F >= MIMO_REGDIET_MINF;
+  constexpr bool E2_RE = (MIMO_REGDIET & 2) && sizeof(R) == 8 && F >= MIMO_REGDIET_MINF;  // |Hhat|^2 after the FFT
+  C symw_r[SYMW_LDS || SYMW_RE ? 1 : NSLOT];
+  uint32_t slab_r[SYMW_RE ? NSLOT : 1];
   auto set_symbols = [&](const uint32_t (&lab_in)[NSLOT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
-      const C v = cscale(qam_point<R>(lab_in[s], L, hb), inv_nrm[s] * inv_sqrt_f);
-      if constexpr (SYMW_LDS) symw_s[s * T + t] = v; else symw_r[s] = v;
+      if constexpr (SYMW_RE) {
+        slab_r[s] = lab_in[s];
+      } else {
+        const C v = cscale(qam_point<R>(lab_in[s], L, hb), inv_nrm[s] * inv_sqrt_f);
+        if constexpr (SYMW_LDS) symw_s[s * T + t] = v; else symw_r[s] = v;
+      }
     }
   };
   auto symw = [&](int s) __attribute__((always_inline)) -> C {
-    if constexpr (SYMW_LDS) return symw_s[s * T + t]; else return symw_r[s];
+    if constexpr (SYMW_RE) {
+      uint32_t l = slab_r[s];
+      R in = inv_nrm[s];
+      asm volatile("" : "+v"(l), "+v"(in));
+      return cscale(qam_point<R>(l, L, hb), in * inv_sqrt_f);
+    } else if constexpr (SYMW_LDS) {
+      return symw_s[s * T + t];
+    } else {
+      return symw_r[s];
+    }
   };
   auto array_pass = [&](bool main_pass, C (&acc)[NSLOT]) __attribute__((always_inline)) {
 #pragma unroll
@@ -829,7 +854,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         const C y = SL::gather(d, s, t0);
         if (main_pass) {
           acc[s] = cmac(acc[s], h[s], y);
-          g[s] = fmar(alpha_a, e2[s], g[s]);  // sum_a alpha_a |Hhat|^2; x 1/||Hhat|| after the pass
+          if constexpr (E2_RE) {
+            C e = hest(s);
+            asm volatile("" : "+v"(e.x), "+v"(e.y));
+            g[s] = fmar(alpha_a, fmar(e.x, e.x, e.y * e.y), g[s]);
+          } else {
+            g[s] = fmar(alpha_a, e2[s], g[s]);  // sum_a alpha_a |Hhat|^2; x 1/||Hhat|| after the pass
+          }
           const C e = hest(s);
           if constexpr (CSI) cc[s] = cadd(cc[s], cscale(cmulc(h[s], e), inv_nrm[s]));
         } else {

@@ -21,6 +21,7 @@ CASES = [
     (8192, 4096, 4, 64, "rapp", 3.0, 3.0, None),     # config-5 FFT / PA, integer-p Rapp path
     (8192, 4096, 4, 16, "rapp", 2.5, 2.0, None),     # general Rapp path
     (8192, 4096, 4, 64, "rapp", 3.0, 3.0, 1024),     # 16-wave team
+    (8192, 2048, 4, 16, "softlim", 0.0, 3.0, None),  # F 8192 generic slots (fp64: S % 4T != 0 at T = 1024)
     (1024, 1000, 8, 16, "softlim", 0.0, 1.0, None),  # generic slots (S % 4T != 0)
     (512, 256, 16, 4, "toi", 0.0, 5.0, None),        # QPSK, cubic PA
     (2048, 1024, 8, 256, "softlim", 0.0, 0.0, None),  # 256-QAM at IBO 0 (strong clipping)
