@@ -66,6 +66,9 @@ constexpr int kMaxCsiAnt = 512;  // CSI-error runs: antennas (LDS per team; engi
 #ifndef MIMO_REGDIET_MINF
 #define MIMO_REGDIET_MINF 8192  // ... from this FFT size (F 8192: -2.1 %; F 2048 bit 1: +0.8 %, off)
 #endif
+#ifndef MIMO_RAWPIPE64
+#define MIMO_RAWPIPE64 0  // fp64 A/B knob: pipeline antenna a+1's Philox words only (see array_pass)
+#endif
 #ifndef MIMO_VK_DPP
 #define MIMO_VK_DPP 1  // per-antenna precoding-power wave sum by DPP (0: __shfl_xor)
 #endif
@@ -432,6 +435,33 @@ struct Channel {
     }
   }
 
+  // Raw-word pipeline (RAWPIPE): the Philox words of chunk c (the counter normals_chunk
+  // uses), and the chunk's normals from those words: chunk_from_words(c, chunk_words(c)) ==
+  // normals_chunk(c) bit for bit.
+  static __device__ __forceinline__ uint4 chunk_words(int c, Key key, uint32_t trial, uint32_t stream, uint32_t aux,
+                                                      int t, int S) {
+    const int j = c >> 1;
+    uint32_t q;
+    if ((c & 1) == 0) q = (j == 0 && t == 0) ? (uint32_t)((S >> 1) - 1) : (uint32_t)((S >> 2) - 1 + t + T * j);
+    else q = (uint32_t)(t + T * j);
+    return philox4x32_10(make_uint4(q, trial, stream, aux), key);
+  }
+  static __device__ __forceinline__ void chunk_from_words(int c, uint4 w, int t, C (&z)[NSLOT], R cs) {
+    if constexpr (ALIGNED) {
+      constexpr int Q = SL::HALF / 2;
+      const int j = c >> 1;
+      const C z1 = box_muller(w.x, w.y, cs), z2 = box_muller(w.z, w.w, cs);
+      if ((c & 1) == 0) {
+        const bool sw = (j == 0) && (t == 0);
+        z[j] = sw ? z2 : z1;
+        z[j + Q] = sw ? z1 : z2;
+      } else {
+        z[SL::HALF + j] = z1;
+        z[SL::HALF + j + Q] = z2;
+      }
+    }
+  }
+
   // |H|^2 of antenna a at the thread's slots (Rayleigh, FSPL factor f_rel left out as in
   // gen<false>): the same draws as gen(), magnitudes only.
   template <class PP>
@@ -746,12 +776,26 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       if (MIMO_ABL(p, ABL_RNG)) CHN::template gen<FREL>(p, key, trial, 0, t, rx, hnext);
       else CHN::normals(key, trial, ST_CHAN, 0u, t, S, hnext, bm_c<R>(sa * sa));
     }
+    // RAWPIPE (fp64 A/B knob): only antenna a+1's Philox words (4 VGPRs per chunk instead
+    // of 8 for its normals) are drawn in antenna a's exchange windows; Box-Muller runs
+    // at the top of antenna a+1.
+    constexpr bool RAWPIPE = MIMO_RAWPIPE64 && !PIPE && sizeof(R) == 8 && ALIGNED && CH == CH_RAYLEIGH && !CSI;
+    uint4 wnext[RAWPIPE ? CHN::kChunks : 1];
+    if constexpr (RAWPIPE) {
+#pragma unroll
+      for (int c = 0; c < CHN::kChunks; ++c) wnext[c] = CHN::chunk_words(c, key, trial, ST_CHAN, 0u, t, S);
+    }
     for (int a = 0; a < A; ++a) {
       const int tl = opaque(t);
       C h[NSLOT];
       if constexpr (PIPE) {
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s) h[s] = hnext[s];
+      } else if constexpr (RAWPIPE) {
+        const R sa = p.ant_rel[a];
+        const R cs = bm_c<R>(sa * sa);
+#pragma unroll
+        for (int c = 0; c < CHN::kChunks; ++c) CHN::chunk_from_words(c, wnext[c], tl, h, cs);
       } else {
         CHN::template gen<FREL>(p, key, trial, a, tl, rx, h);
       }
@@ -763,6 +807,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       // splits the exchange windows' basic blocks; profiles/r02/ab/ab32_lastant.json).
       // Ablation ABL_RNG: antenna a+1's synthetic channel, in window 0.
       auto hfill = [&](int w) __attribute__((always_inline)) {
+        if constexpr (RAWPIPE) {
+          constexpr int NC = CHN::kChunks, NW = 2 * FFT::XCHG;
+#pragma unroll
+          for (int c = 0; c < NC; ++c)
+            if (c >= w * NC / NW && c < (w + 1) * NC / NW)
+              wnext[c] = CHN::chunk_words(c, key, trial, ST_CHAN, (uint32_t)an, tl, S);
+        }
         if constexpr (PIPE) {
           constexpr int NC = CHN::kChunks, NW = 2 * FFT::XCHG;
           if (MIMO_ABL(p, ABL_RNG)) {
