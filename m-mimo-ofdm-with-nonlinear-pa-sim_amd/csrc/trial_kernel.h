@@ -22,8 +22,8 @@
 //
 // Without CSI errors the per-sub-carrier FSPL ratio f_c/f_k is factored out of the
 // antenna loops (it cancels in MRT) and the per-antenna ratio is folded into the
-// Box-Muller radius; alpha_a comes from a host-fitted polynomial (F <= 4096).  The
-// kernel is fp32-VALU-issue-bound.
+// Box-Muller radius; alpha_a comes from a host-fitted polynomial (fp32, F <= 4096) or a
+// Chebyshev series (fp64).  Both instances are VALU-issue-bound.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
