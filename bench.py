@@ -4,9 +4,10 @@ Workload (BASELINE.json configs[1]): 64-antenna MRT, 1024 sub-carriers (FFT 2048
 soft-limiter PA at IBO 3 dB, i.i.d. Rayleigh channel rerolled per trial, Eb/N0 15 dB,
 standard receiver (iteration 0), 2^16 trials (= OFDM symbols) per step.  One step = one
 fused-kernel launch over the batch + the on-device count reduction.  Inputs are generated
-on the device from Philox streams (no host transfer).  ``--gpus N`` (torchrun, one rank
-per GPU) shards trials by index: weak scaling, no data-path collective; the per-step
-error counts are summed across ranks once at the end (RCCL all_reduce).
+on the device from Philox streams (no host transfer).  ``--gpus N`` (one rank per GPU,
+under torchrun; without an outer torchrun the script starts it as a child process)
+shards trials by index: weak scaling, no data-path collective; the per-step error counts
+are summed across ranks once at the end (RCCL all_reduce).
 
 Prints ONE JSON line (rank 0).
 """
@@ -59,6 +60,14 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # (157.3 TF, VALU == MFMA f32).  f64: AMD's MI355X spec sheet (78.6 TF vector; the guide
 # lists no f64 figure) -- the fused kernel issues no MFMA, so the VALU peak is the ceiling.
 VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}
+
+
+# The reference's own Link.simulate (NumPy + torch CPU FFT, numba absent) timed in the build
+# container (SURVEY.md §6, config-2 geometry, standard RX): it cannot travel to the GPU box,
+# so the bench line quotes it beside the measured port.
+CPU_REFERENCE_SURVEY = {"per_process": 5.7, "n8_processes": 35.8, "unit": "OFDM symbols/s", "cores": 8,
+                        "kind": "reference", "source": "SURVEY.md §6 (Intel Xeon, 8 cores, mp.Process x 8 as "
+                                                      "main_mp_miso_cnc_ber_vs_ebn0.py:122-132)"}
 
 
 def bytes_alg_per_trial(a=A, s=S, f=F):
@@ -169,9 +178,12 @@ def cpu_baseline(seconds=15.0, workload="2", iters=(0,), cores=None):
     busy = max(r[1] for r in res)
     w = WORKLOADS[workload]
     rx = ("MCNC" if w.get("mcnc") else "CNC") + f" iterations {iters}" if iters != [0] else "standard RX"
-    return dict(value=round(n / busy, 3), unit="OFDM symbols/s", cores=cores, kind="port",
-                sample=f"{n} trials of the workload-{workload} chain ({rx}) through oracle/sim.py (NumPy float64), "
-                       f"{cores} spawned processes x {busy:.1f} s each (pool wall {wall:.1f} s incl. start-up)")
+    out = dict(value=round(n / busy, 3), unit="OFDM symbols/s", cores=cores, kind="port",
+               sample=f"{n} trials of the workload-{workload} chain ({rx}) through oracle/sim.py (NumPy float64), "
+                      f"{cores} spawned processes x {busy:.1f} s each (pool wall {wall:.1f} s incl. start-up)")
+    if workload == "2":
+        out["cpu_reference_published"] = CPU_REFERENCE_SURVEY
+    return out
 
 
 def load_pmc_traffic(workload, iters, precision, trials_per_launch):
@@ -189,6 +201,39 @@ def load_pmc_traffic(workload, iters, precision, trials_per_launch):
     return None, None
 
 
+def launch_ranks(n):
+    """``--gpus N`` without an outer torchrun: start ``torch.distributed.run`` with N ranks
+    as a CHILD process (this parent has made no GPU call and never execs), forward rank 0's
+    JSON line and return the child's exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    for line in proc.stdout.splitlines():
+        if line.startswith("{"):
+            print(line, flush=True)
+        else:
+            print(line, file=sys.stderr, flush=True)
+    return proc.returncode
+
+
+def check_launch(world, rank):
+    """``--check-launch``: the rank plumbing only (process group over gloo, the world size
+    the driver asked for, one all_reduce); no engine, no GPU.  For the CPU launcher test."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"check": "launch", "n_gpus": world, "ranks_seen": int(t.item())}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -202,11 +247,19 @@ def main():
                     help="arithmetic type of the fused kernel (f64 = the reference's float64)")
     ap.add_argument("--workload", default="2", choices=sorted(WORKLOADS),
                     help="2 = BASELINE config 2 (headline); paper; 5su (config-5 array, one user)")
+    ap.add_argument("--check-launch", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    if args.check_launch:
+        return check_launch(world, rank)
     import torch
     dist = None
     # MIMO_BENCH_BACKEND=gloo rehearses the N > 1 path with ranks sharing the visible GPUs

@@ -546,8 +546,9 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
   }
   const mimo::InstanceKey key = select_instance(e, csi);
   if (int rc = ensure_device(e)) return rc;
-  if (!c.reroll_chan && c.channel_kind != MIMO_CH_RAYLEIGH) {
+  if (!c.reroll_chan && (c.channel_kind == MIMO_CH_LOS || c.channel_kind == MIMO_CH_TWOPATH)) {
     // fixed RX: jitter span 0 around (x0, x0); only consistent when rx_y == rx_x
+    // (table channels never use the RX position)
     if (c.rx_pos[1] != c.rx_pos[0]) return fail(MIMO_EINVAL, "reroll_chan=0 requires rx_pos[1] == rx_pos[0]");
   }
   char buf[160];
@@ -667,6 +668,7 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
         }
       }
       const uint32_t nb = start[nseg];
+      if (nb == 0) continue;  // every point of the call has n_trials == 0: nothing to launch
       TP kp = base;
       kp.points = reinterpret_cast<const TP*>(e->d_blob);
       kp.point_start = reinterpret_cast<const uint32_t*>(e->d_blob + o_start);

@@ -77,82 +77,11 @@ __device__ __forceinline__ double log2_r(double x) { return log2(x); }
 __device__ __forceinline__ double exp2_r(double x) { return exp2(x); }
 __device__ __forceinline__ double rcp_r(double x) { return 1.0 / x; }
 
-// Natural log of a positive normal double: x = m 2^e with m in [sqrt(1/2), sqrt(2)),
-// ln m = 2 atanh(s), s = (m - 1) / (m + 1), |s| <= 0.1716: the series to s^19 is below
-// 2^-54 relative.  ~25 VALU ops; <= 2 ulp.
-__device__ __forceinline__ double ln_pos(double x) {
-  int e = __builtin_amdgcn_frexp_exp(x);
-  double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
-  const bool lo = m < 0.70710678118654752440;
-  m = lo ? m + m : m;
-  e = lo ? e - 1 : e;
-  const double f = m - 1.0;
-  const double den = 2.0 + f;
-  double r = __builtin_amdgcn_rcp(den);  // Newton: r (2 - den r), twice
-  r = fma(r, fma(-den, r, 1.0), r);
-  r = fma(r, fma(-den, r, 1.0), r);
-  const double s = f * r;
-  const double z = s * s;
-  double q = 2.0 / 19;
-  q = fma(q, z, 2.0 / 17);
-  q = fma(q, z, 2.0 / 15);
-  q = fma(q, z, 2.0 / 13);
-  q = fma(q, z, 2.0 / 11);
-  q = fma(q, z, 2.0 / 9);
-  q = fma(q, z, 2.0 / 7);
-  q = fma(q, z, 2.0 / 5);
-  q = fma(q, z, 2.0 / 3);
-  const double lnm = fma(s * z, q, s + s);
-  constexpr double kLn2Hi = 6.93147180369123816490e-01;  // ln 2 with 21 trailing zero bits
-  constexpr double kLn2Lo = 1.90821492927058770002e-10;
-  const double de = (double)e;
-  return fma(de, kLn2Hi, fma(de, kLn2Lo, lnm));
-}
-
-// sin / cos of 2 pi r (r in revolutions, |r| < 2^20): quadrant n = rint(4 r) is split
-// off exactly (Sterbenz), phi = 2 pi (r - n/4) in [-pi/4, pi/4], Taylor to phi^15 / phi^16
-// (truncation < 0.6 ulp).  The fp32 kernel's v_sin / v_cos also take revolutions.
-__device__ __forceinline__ void sincos_rev(double r, double& sn, double& cs) {
-  const double n = __builtin_rint(4.0 * r);
-  const double phi = (r - 0.25 * n) * 6.28318530717958647693;
-  const double z = phi * phi;
-  double ps = -1.0 / 1307674368000.0;         // -1/15!
-  ps = fma(ps, z, 1.0 / 6227020800.0);        // 1/13!
-  ps = fma(ps, z, -1.0 / 39916800.0);         // -1/11!
-  ps = fma(ps, z, 1.0 / 362880.0);            // 1/9!
-  ps = fma(ps, z, -1.0 / 5040.0);
-  ps = fma(ps, z, 1.0 / 120.0);
-  ps = fma(ps, z, -1.0 / 6.0);
-  const double s = fma(phi * z, ps, phi);
-  double pc = 1.0 / 20922789888000.0;         // 1/16!
-  pc = fma(pc, z, -1.0 / 87178291200.0);      // -1/14!
-  pc = fma(pc, z, 1.0 / 479001600.0);         // 1/12!
-  pc = fma(pc, z, -1.0 / 3628800.0);          // -1/10!
-  pc = fma(pc, z, 1.0 / 40320.0);
-  pc = fma(pc, z, -1.0 / 720.0);
-  pc = fma(pc, z, 1.0 / 24.0);
-  pc = fma(pc, z, -0.5);
-  const double c = fma(z, pc, 1.0);
-  const int q = ((int)n) & 3;
-  // (sin, cos) of phi + q pi/2
-  const double s1 = (q & 1) ? c : s, c1 = (q & 1) ? s : c;
-  sn = (q & 2) ? -s1 : s1;
-  cs = ((q + 1) & 2) ? -c1 : c1;
-}
-__device__ __forceinline__ double sin_rev(double r) {
-  double s, c;
-  sincos_rev(r, s, c);
-  return s;
-}
-__device__ __forceinline__ double cos_rev(double r) {
-  double s, c;
-  sincos_rev(r, s, c);
-  return c;
-}
 // ---------------------------------------------------------------- fp64: table-driven forms
 // The fp64 trial kernel's Box-Muller draws (2 A S normals per trial) dominate its
 // transcendental work, so they use LDS tables instead of the long series above
-// (ln: ~13 f64 ops instead of ~25 plus a Newton reciprocal; sincos: ~15 instead of ~35).
+// (ln: ~13 f64 ops instead of ~25 plus a Newton reciprocal for the atanh series; sincos:
+// ~15 instead of ~35 for a quadrant Taylor series; the series forms are in git history).
 // Table (host-built, engine.hip lut64_table, loaded into LDS at kernel start):
 //   [0, 512):   (c_i, -ln c_i) for m in bucket i of [sqrt(1/2), sqrt(2)) (i = bit 20..12 of
 //               the high word of m: exponent LSB + 8 mantissa bits); c_i ~ 1/centre_i rounded

@@ -22,27 +22,6 @@
 
 #include "real.h"
 
-#ifndef MIMO_DIAG_NOPREBAR
-#define MIMO_DIAG_NOPREBAR 0  // timing diagnostics only (wrong results); production = 0
-#endif
-#ifndef MIMO_DIAG_NOTW
-#define MIMO_DIAG_NOTW 0
-#endif
-#ifndef MIMO_TW_LOAD_MAX
-#define MIMO_TW_LOAD_MAX 64  // twiddle powers r <= this are loaded (1: square the rest; measured neutral)
-#endif
-#ifndef MIMO_TW_LOAD_ALL
-#define MIMO_TW_LOAD_ALL 0  // 1: load every twiddle power (no products; A/B knob)
-#endif
-#ifndef MIMO_TW_PREFETCH
-#define MIMO_TW_PREFETCH 1  // load every stage's base twiddles at the start of a transform (F <= 4096)
-#endif
-#ifndef MIMO_PADN_SHIFT
-#define MIMO_PADN_SHIFT 5  // padding of exchanges >= 1
-#endif
-#ifndef MIMO_PAD0_SHIFT
-#define MIMO_PAD0_SHIFT 4
-#endif
 
 namespace mimo {
 
@@ -69,20 +48,17 @@ constexpr int ilog2(int n) { return n <= 1 ? 0 : 1 + ilog2(n >> 1); }
 // jm < NS, 1 <= r < R, stored per stage as a [R][NS] block (lane-contiguous in jm) of
 // one table; fft_tw_off(s) is the block's offset.
 constexpr int fft_nst(int F, int P) { return (ilog2(F) + ilog2(P) - 1) / ilog2(P); }
-// Radix plan.  MIMO_FFT_PLAN 1: the last stage has radix P (one butterfly per thread,
-// NS = T), the other bits are spread front-loaded over the earlier stages.  Every stage
-// then has NS <= T, so the twiddles of a thread's butterflies i > 0 equal those of
-// butterfly 0 (no compile-time rotations), e.g. F = 2048, P = 16: 16 x 8 x 16.
-// Plan 0: front-loaded (16 x 16 x 8; the last stage's second butterfly rotates).
-#ifndef MIMO_FFT_PLAN
-#define MIMO_FFT_PLAN 1
-#endif
+// Radix plan: the last stage has radix P (one butterfly per thread, NS = T), the other
+// bits are spread front-loaded over the earlier stages.  Every stage then has NS <= T, so
+// the twiddles of a thread's butterflies i > 0 equal those of butterfly 0 (no compile-time
+// rotations), e.g. F = 2048, P = 16: 16 x 8 x 16.  (The front-loaded 16 x 16 x 8 plan,
+// whose last stage's second butterfly rotates, measured slower: git history.)
 constexpr int fft_bits(int F, int P, int s) {
-  if (MIMO_FFT_PLAN == 1 && fft_nst(F, P) > 1) {
+  if (fft_nst(F, P) > 1) {
     const int n = fft_nst(F, P) - 1, rest = ilog2(F) - ilog2(P);
     return s == n ? ilog2(P) : rest / n + (s < rest % n ? 1 : 0);
   }
-  return ilog2(F) / fft_nst(F, P) + (s < ilog2(F) % fft_nst(F, P) ? 1 : 0);
+  return ilog2(F);
 }
 constexpr int fft_bits_before(int F, int P, int s) { return s == 0 ? 0 : fft_bits_before(F, P, s - 1) + fft_bits(F, P, s - 1); }
 constexpr int fft_tw_off(int F, int P, int s) {
@@ -247,16 +223,17 @@ struct TeamFft {
   static constexpr int LOG_P = ilog2(P);
   static constexpr int NST = fft_nst(F, P);
   // Padding of exchange S: one slot per 2^PSH elements.  Exchange 0 (stage 0 writes
-  // 16t + r) uses 1/16 (MIMO_PAD0_SHIFT): it halves that exchange's modelled bank
+  // 16t + r) uses 1/16: it halves that exchange's modelled bank
   // conflicts (tools/lds_conflicts.py); later exchanges use 1/32.
   // fp64 elements are 16 B (ds_write_b128: 8-lane groups over 32 banks), where stage 0's
   // stride-R writes need one pad slot per 8 elements: the modelled extra LDS cycles of
   // exchange 0 drop 3x (tools/lds_conflicts.py; the model reproduces SQ_LDS_BANK_CONFLICT
   // of the 1/16 layout exactly, profiles/r02/pmc_f64_r1).  F = 8192 keeps 1/16: its 16 KiB
   // more would not fit the 160 KiB LDS next to the fp64 tables and the CSI scratch.
-  static constexpr int PAD0 = (sizeof(Re) == 8 && F < 8192) ? 3 : MIMO_PAD0_SHIFT;
-  static constexpr int psh(int S) { return S == 0 ? PAD0 : MIMO_PADN_SHIFT; }
-  static constexpr int LDS_ELEMS = F + F / (1 << (PAD0 < MIMO_PADN_SHIFT ? PAD0 : MIMO_PADN_SHIFT));
+  static constexpr int PADN = 5;  // one pad slot per 32 elements for exchanges >= 1
+  static constexpr int PAD0 = (sizeof(Re) == 8 && F < 8192) ? 3 : 4;
+  static constexpr int psh(int S) { return S == 0 ? PAD0 : PADN; }
+  static constexpr int LDS_ELEMS = F + F / (1 << (PAD0 < PADN ? PAD0 : PADN));
   static_assert((1 << LOG_F) == F && (1 << LOG_P) == P && P >= 2, "power-of-two sizes");
   static_assert(!WAVE || T == 64, "wave-local transforms are one wave");
 
@@ -266,11 +243,6 @@ struct TeamFft {
   static __host__ __device__ constexpr int pad(int e) { return e + (e >> psh(S)); }
   // Global-address-space load (the laundered table pointer would otherwise be generic
   // and compile to flat loads, which also count against lgkmcnt with the LDS traffic).
-  static __device__ __forceinline__ C opaque_tw(int r) {
-    C w = mkc(Re(0.6), Re(0.8) * (Re)(r & 1));
-    asm volatile("" : "+v"(w.x), "+v"(w.y));
-    return w;
-  }
   static __device__ __forceinline__ C gload(const C* p, int i) {
     typedef Re v2f __attribute__((ext_vector_type(2)));
     const v2f v = ((const __attribute__((address_space(1))) v2f*)p)[i];
@@ -331,7 +303,7 @@ struct TeamFft {
       // One buffer: everyone must have read the previous exchange before it is
       // overwritten.  The barrier sits after this stage's twiddle loads and DFT, so
       // their latency overlaps the previous exchange's reads.
-      if constexpr (NBUF == 1 && I == 0 && !MIMO_DIAG_NOPREBAR) xchg_sync<WAVE>();
+      if constexpr (NBUF == 1 && I == 0) xchg_sync<WAVE>();
       // pad(base + r NS) == pad(base) + pad(r NS) for power-of-two NS, R, T (the
       // padding never splits a write group): one address per i, immediate offsets.
       C* wb = buf + pad<S>((j / NS) * NS * R + jm);
@@ -362,17 +334,13 @@ struct TeamFft {
   // log2 R - 1 roundings).  Loads, not multiplies, were the twiddles' cost: dropping the
   // loads saved 17 % of the kernel, dropping the multiplies 8 % (profiles/r01).
   // Base twiddles w(jm0, 2^b) of every stage >= 1, loaded together at the start of a
-  // transform (MIMO_TW_PREFETCH): their L2 latency then overlaps stage 0 and the first
+  // transform (PREFETCH): their L2 latency then overlaps stage 0 and the first
   // exchange instead of stalling each stage's first twiddle multiply.
   static constexpr int kMaxB = 5;
-  // Measured -1.1 % (F 2048), -1.5 % (F 4096), +0.9 % (F 8192: more stages held live).
-  // fp64: off (the prefetched twiddles would hold ~32 more VGPRs across a transform).
-  // fp64: -2.4 % at F = 2048 (with the channel pipeline off, below), +1.5 % at F = 4096
+  // Measured -1.1 % (F 2048), -1.5 % (F 4096), +0.9 % (F 8192: more stages held live);
+  // fp64: -2.4 % at F = 2048 (with the channel pipeline off), +1.5 % at F = 4096
   // (profiles/r02/ab/ab64_*.json).
-#ifndef MIMO_TW_PREFETCH64
-#define MIMO_TW_PREFETCH64 (F <= 2048)
-#endif
-  static constexpr bool PREFETCH = MIMO_TW_PREFETCH && F <= 4096 && (sizeof(Re) == 4 || MIMO_TW_PREFETCH64);
+  static constexpr bool PREFETCH = F <= 4096 && (sizeof(Re) == 4 || F <= 2048);
   // Base holds w(2^k) for k < kMaxB; a stage reads k < bits(S) <= LOG_P.
   static_assert(!PREFETCH || LOG_P <= kMaxB, "Base too small for the plan's largest radix");
   struct Base {
@@ -387,7 +355,7 @@ struct TeamFft {
         constexpr int TW_OFF = fft_tw_off(F, P, S);
         const int jm0 = t & (NS - 1);
 #pragma unroll
-        for (int k = 0; k < bits(S) && k < kMaxB && (1 << k) <= MIMO_TW_LOAD_MAX; ++k)
+        for (int k = 0; k < bits(S) && k < kMaxB; ++k)
           b.v[S][k] = gload(tw + TW_OFF + (1 << k) * NS, jm0);
         (void)R;
       }
@@ -409,7 +377,7 @@ struct TeamFft {
 #pragma unroll
       for (int r = 1; r < R; ++r) {
         if ((r & (r - 1)) == 0) {
-          w0[r] = r <= MIMO_TW_LOAD_MAX ? base.v[S][ilog2(r)] : cmul(w0[r / 2], w0[r / 2]);
+          w0[r] = base.v[S][ilog2(r)];
         } else {
           int hb = r;
           while (hb & (hb - 1)) hb &= hb - 1;
@@ -422,12 +390,7 @@ struct TeamFft {
       const int jm0 = t & (NS - 1);
 #pragma unroll
       for (int r = 1; r < R; ++r) {
-        if (r == 1 || ((r & (r - 1)) == 0 && r > MIMO_TW_LOAD_MAX)) {
-          w0[r] = r > 1 ? cmul(w0[r / 2], w0[r / 2])  // w(2r) = w(r)^2
-                  : MIMO_DIAG_NOTW == 1 ? mkc(Re(1), Re(0))  // diagnostic: no twiddle traffic
-                  : MIMO_DIAG_NOTW == 2 ? opaque_tw(r)            // diagnostic: multiplies, no loads
-                                        : gload(tws + r * NS, jm0);
-        } else if ((r & (r - 1)) == 0 || MIMO_TW_LOAD_ALL) {
+        if ((r & (r - 1)) == 0) {
           w0[r] = gload(tws + r * NS, jm0);
         } else {
           int hb = r;

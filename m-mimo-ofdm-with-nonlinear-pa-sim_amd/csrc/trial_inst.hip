@@ -20,28 +20,15 @@ namespace {
 constexpr int kF = INST_F;
 constexpr bool kF64 = INST_F64 != 0;
 using Real = std::conditional_t<kF64, double, float>;
-#ifndef MIMO_TWOPATH_W2
-#define MIMO_TWOPATH_W2 0  // 1: two-path at 2 waves/SIMD (measured 12 % slower than 3)
-#endif
-#ifndef MIMO_F64_MINW
-#define MIMO_F64_MINW 2  // fp64 instances: waves/SIMD target, exchange buffers, symbols in LDS
-#endif
-#ifndef MIMO_F64_NBUF
-#define MIMO_F64_NBUF 1
-#endif
-#ifndef MIMO_F64_SYMW
-#define MIMO_F64_SYMW 1
-#endif
-#ifndef MIMO_MINW16
-#define MIMO_MINW16 3  // waves/SIMD target of the 16-point aligned instances (A/B knob)
-#endif
 
 // Occupancy profile per instance (see trial_kernel): waves/SIMD target, exchange buffers,
 // symbols in LDS.  Measured on MI355X (tools/ab_libs.py, profiles/r01/ab_*.json):
+//  - fp64 below F = 8192: 2 waves/SIMD (255 VGPRs), one exchange buffer, the weighted
+//    symbols in LDS (F = 2048: 65 KiB / team, 2 teams per CU).
 //  - aligned, 16 points/thread, F <= 4096: 3 waves/SIMD needs <= 168 VGPRs and
 //    <= 160 KiB / (3 waves x 4 SIMD / waves per team) of LDS -> one exchange buffer and
-//    the weighted symbols in LDS (F = 2048: 25 KiB / team).  Two-path channels need
-//    too many registers for it (spills) and stay at 2.
+//    the weighted symbols in LDS (F = 2048: 25 KiB / team).  (Two-path at 2 waves/SIMD
+//    measured 12 % slower.)
 //  - aligned, 8 points/thread: 4 waves/SIMD fit in 128 VGPRs with two buffers.
 //  - generic (unaligned band), 16 slots/thread: symbols in LDS to limit spills.
 struct Profile {
@@ -51,11 +38,10 @@ struct Profile {
 constexpr Profile profile_for(int T, bool aligned, int ch) {
   const int P = kF / T;
   if (kF64 && kF >= 8192) return Profile{2, 1, false};  // 136 KiB exchange buffer: one team per CU (T = 1024: 4 waves/SIMD)
-  if (kF64) return Profile{MIMO_F64_MINW, MIMO_F64_NBUF, MIMO_F64_SYMW != 0};
+  if (kF64) return Profile{2, 1, true};
   if (!aligned) return Profile{2, kF >= 4096 ? 1 : 2, true};  // one buffer from F = 4096: 2 teams/CU
-  if (ch == CH_TWOPATH && MIMO_TWOPATH_W2) return Profile{2, 2, false};  // fp64 geometry: register-heavy
   if (P < 16) return Profile{4, 2, false};
-  if (kF <= 4096) return Profile{MIMO_MINW16, MIMO_MINW16 == 3 ? 1 : 2, MIMO_MINW16 == 3};
+  if (kF <= 4096) return Profile{3, 1, true};
   return Profile{2, 2, false};
 }
 

@@ -42,36 +42,10 @@ enum RxKind : int { RX_CNC = 1, RX_MCNC = 2 };
 
 constexpr int kMaxWaves = 16;
 constexpr int kMaxCsiAnt = 512;  // CSI-error runs: antennas (LDS per team; engine.hip checks)
-#ifndef MIMO_RAPP_INT
-#define MIMO_RAPP_INT 1   // A/B knobs (Makefile target variant); production defaults
-#endif
-#ifndef MIMO_PASS1_POW
-#define MIMO_PASS1_POW 1
-#endif
-#ifndef MIMO_ALPHA_POLY
-#define MIMO_ALPHA_POLY 1
-#endif
-#ifndef MIMO_ALPHA_CHEB64
-#define MIMO_ALPHA_CHEB64 1  // fp64: Chebyshev alpha (A/B knob; 0 = library exp / erfc every antenna)
-#endif
-#ifndef MIMO_HPIPE
-#define MIMO_HPIPE 1  // draw antenna a+1's channel inside antenna a's FFT exchanges (aligned Rayleigh)
-#endif
-#ifndef MIMO_HPIPE64_OFF_F
-#define MIMO_HPIPE64_OFF_F 8192  // fp64: no channel pipeline up to this FFT size (A/B knob; F 4096: -2.3 %, F 8192: -20 %)
-#endif
-#ifndef MIMO_REGDIET
-#define MIMO_REGDIET 3  // fp64 register diet: bit 0 symbols rebuilt per antenna, bit 1 |H|^2 recomputed
-#endif
-#ifndef MIMO_REGDIET_MINF
-#define MIMO_REGDIET_MINF 8192  // ... from this FFT size (F 8192: -2.1 %; F 2048 bit 1: +0.8 %, off)
-#endif
-#ifndef MIMO_RAWPIPE64
-#define MIMO_RAWPIPE64 0  // fp64 A/B knob: pipeline antenna a+1's Philox words only (see array_pass)
-#endif
-#ifndef MIMO_VK_DPP
-#define MIMO_VK_DPP 1  // per-antenna precoding-power wave sum by DPP (0: __shfl_xor)
-#endif
+constexpr uint32_t kFixedCsiTrial = 0xFFFFFFFFu;  // CSI stream counter of fixed-channel runs (oracle/sim.py draws)
+// The measured alternatives of the choices below (channel pipeline on / off per precision,
+// register diet from F 8192, raw-word pipeline, alpha by library exp / erfc, shfl vs DPP
+// sums) are in DESIGN.md §3 and profiles/r02/ab/; the losing variants were removed.
 
 template <typename R>
 struct TrialParams {
@@ -306,12 +280,10 @@ __device__ __forceinline__ void pa_block(int kind, C (&d)[P], R sat, R sqrt_sat,
   if (kind == PA_SOFTLIM) {
 #pragma unroll
     for (int m = 0; m < P; ++m) d[m] = pa_apply(PA_SOFTLIM, d[m], sat, sqrt_sat, inv_sat, rapp_p, toi);
-#if MIMO_RAPP_INT
   } else if (kind == PA_RAPP && rapp_p == R(3)) {
     rapp_int<3>(d, inv_sat);
   } else if (kind == PA_RAPP && rapp_p == R(2)) {
     rapp_int<2>(d, inv_sat);
-#endif
   } else if (kind == PA_RAPP) {
 #pragma unroll
     for (int m = 0; m < P; ++m) d[m] = pa_apply(PA_RAPP, d[m], sat, sqrt_sat, inv_sat, rapp_p, toi);
@@ -354,14 +326,13 @@ __device__ __forceinline__ cx<R> qam_point(uint32_t label, int L, int hb) {
 
 // ---------------------------------------------------------------- channel generation
 // sin / cos of a channel phase in revolutions: fp32 hardware (v_sin / v_cos take
-// revolutions), fp64 the table form (real.h sincos_rev_lut; MIMO_SC_LUT = 0: the series).
+// revolutions), fp64 the table form (real.h sincos_rev_lut).
 __device__ __forceinline__ void sincos_phase(float r, float& sn, float& cs) {
   sn = sin_rev(r);
   cs = cos_rev(r);
 }
 __device__ __forceinline__ void sincos_phase(double r, double& sn, double& cs) {
-  if constexpr (MIMO_SC_LUT) sincos_rev_lut(r, sn, cs);
-  else sincos_rev(r, sn, cs);
+  sincos_rev_lut(r, sn, cs);
 }
 
 template <typename R, int F, int T, int NSLOT, bool ALIGNED, int CH>
@@ -429,33 +400,6 @@ struct Channel {
         z[j + Q] = sw ? z1 : z2;
       } else {
         cn_pair(key, (uint32_t)(t + T * j), trial, stream, aux, z1, z2, cs);
-        z[SL::HALF + j] = z1;
-        z[SL::HALF + j + Q] = z2;
-      }
-    }
-  }
-
-  // Raw-word pipeline (RAWPIPE): the Philox words of chunk c (the counter normals_chunk
-  // uses), and the chunk's normals from those words: chunk_from_words(c, chunk_words(c)) ==
-  // normals_chunk(c) bit for bit.
-  static __device__ __forceinline__ uint4 chunk_words(int c, Key key, uint32_t trial, uint32_t stream, uint32_t aux,
-                                                      int t, int S) {
-    const int j = c >> 1;
-    uint32_t q;
-    if ((c & 1) == 0) q = (j == 0 && t == 0) ? (uint32_t)((S >> 1) - 1) : (uint32_t)((S >> 2) - 1 + t + T * j);
-    else q = (uint32_t)(t + T * j);
-    return philox4x32_10(make_uint4(q, trial, stream, aux), key);
-  }
-  static __device__ __forceinline__ void chunk_from_words(int c, uint4 w, int t, C (&z)[NSLOT], R cs) {
-    if constexpr (ALIGNED) {
-      constexpr int Q = SL::HALF / 2;
-      const int j = c >> 1;
-      const C z1 = box_muller(w.x, w.y, cs), z2 = box_muller(w.z, w.w, cs);
-      if ((c & 1) == 0) {
-        const bool sw = (j == 0) && (t == 0);
-        z[j] = sw ? z2 : z1;
-        z[j + Q] = sw ? z1 : z2;
-      } else {
         z[SL::HALF + j] = z1;
         z[SL::HALF + j + Q] = z2;
       }
@@ -626,6 +570,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   const int lane = t & 63, wid = t >> 6;
   const uint32_t trial = (uint32_t)(p.first_trial + (blockIdx.x - p0.point_start[pi]));
   const Key key{(uint32_t)p.seed, (uint32_t)(p.seed >> 32)};
+  // CSI error draws: per trial with a rerolled channel (set_precoding_and_recalculate_agc
+  // per trial, mp_model.py:206); with a fixed channel (CH_TABLE, reroll_chan=False) the
+  // reference draws the erroneous estimate once (Link.__init__, mp_model.py:87) and keeps
+  // it for every trial, so all trials share one draw (trial-independent counter).
+  const uint32_t csi_trial = CH == CH_TABLE ? kFixedCsiTrial : trial;
   const int S = p.n_sc, A = p.n_ant, L = p.qam_l, hb = p.half_bits;
   const R inv_sqrt_f = p.inv_sqrt_f;
   if constexpr (sizeof(R) == 8) {  // Box-Muller tables (real.h ln_lut / sincos_lut) into LDS
@@ -677,7 +626,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   for (int s = 0; s < NSLOT; ++s) nrm2[s] = R(0);
   for (int a = 0; a < (MIMO_ABL(p, ABL_PASS1) ? 1 : A); ++a) {
     const int tl = opaque(t);
-    if constexpr (CH == CH_RAYLEIGH && !CSI && MIMO_PASS1_POW) {
+    if constexpr (CH == CH_RAYLEIGH && !CSI) {
       if (!MIMO_ABL(p, ABL_RNG)) {
         R e2[NSLOT];
         CHN::power(p, key, trial, a, tl, e2);
@@ -696,7 +645,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       pw = team_sum<T>(pw, red) / (R)S;
       if (t0) pw_csi[a] = pw;
       C zc[NSLOT];
-      CHN::normals(key, trial, ST_CSI, (uint32_t)a, tl, S, zc);
+      CHN::normals(key, csi_trial, ST_CSI, (uint32_t)a, tl, S, zc);
       const R sc = p.csi_b * sqrt_ieee(pw);
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s)
@@ -731,11 +680,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // MAIN: symbols = tx labels, combine with the true channel, accumulate g (alpha_a).
   // MCNC: symbols = detected labels, combine with the estimated channel (corrector.py:198-200).
   // The symbols enter pre-weighted, symw = s / ||Hhat|| / sqrt(F) (0 on invalid slots).
-  // SYMW_RE (register diet, MIMO_REGDIET bit 0, symbols not in LDS): keep the labels
+  // SYMW_RE (register diet, symbols not in LDS): keep the labels
   // (1 VGPR per slot) and rebuild the symbol per antenna instead of holding it (4 VGPRs
   // in fp64); the opaque copies stop the compiler from hoisting it back out of the loop.
-  constexpr bool SYMW_RE = !SYMW_LDS && (MIMO_REGDIET & 1) && sizeof(R) == 8 && F >= MIMO_REGDIET_MINF;
-  constexpr bool E2_RE = (MIMO_REGDIET & 2) && sizeof(R) == 8 && F >= MIMO_REGDIET_MINF;  // |Hhat|^2 after the FFT
+  // Register diet of the fp64 F = 8192 instance (-2.1 %; at F 2048 the |Hhat|^2 half measured
+  // +0.8 %): symbols rebuilt from the labels per antenna, |Hhat|^2 recomputed after the FFT.
+  constexpr bool SYMW_RE = !SYMW_LDS && sizeof(R) == 8 && F >= 8192;
+  constexpr bool E2_RE = sizeof(R) == 8 && F >= 8192;
   C symw_r[SYMW_LDS || SYMW_RE ? 1 : NSLOT];
   uint32_t slab_r[SYMW_RE ? NSLOT : 1];
   auto set_symbols = [&](const uint32_t (&lab_in)[NSLOT]) __attribute__((always_inline)) {
@@ -769,21 +720,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     // fp64 at F <= 4096: off (the pipelined draws' registers cost more than the exchange
     // windows hide: -1.8 % without at F 2048, profiles/r02/ab/ab64_2048.json; -2.3 % at
     // F 4096 with the wave-split FFT, scratch 140 -> 36 B/lane, profiles/r02/ab/ab4k_pipe_off.json).
-    constexpr bool PIPE = MIMO_HPIPE && ALIGNED && CH == CH_RAYLEIGH && !CSI && !(sizeof(R) == 8 && F <= MIMO_HPIPE64_OFF_F);
+    // fp64 at F 8192: -20 % without (profiles/r02/ab/ab8k_f64_team_pipe.json): fp64 never pipelines.
+    constexpr bool PIPE = ALIGNED && CH == CH_RAYLEIGH && !CSI && sizeof(R) == 4;
     C hnext[PIPE ? NSLOT : 1];
     if constexpr (PIPE) {
       const R sa = p.ant_rel[0];
       if (MIMO_ABL(p, ABL_RNG)) CHN::template gen<FREL>(p, key, trial, 0, t, rx, hnext);
       else CHN::normals(key, trial, ST_CHAN, 0u, t, S, hnext, bm_c<R>(sa * sa));
-    }
-    // RAWPIPE (fp64 A/B knob): only antenna a+1's Philox words (4 VGPRs per chunk instead
-    // of 8 for its normals) are drawn in antenna a's exchange windows; Box-Muller runs
-    // at the top of antenna a+1.
-    constexpr bool RAWPIPE = MIMO_RAWPIPE64 && !PIPE && sizeof(R) == 8 && ALIGNED && CH == CH_RAYLEIGH && !CSI;
-    uint4 wnext[RAWPIPE ? CHN::kChunks : 1];
-    if constexpr (RAWPIPE) {
-#pragma unroll
-      for (int c = 0; c < CHN::kChunks; ++c) wnext[c] = CHN::chunk_words(c, key, trial, ST_CHAN, 0u, t, S);
     }
     for (int a = 0; a < A; ++a) {
       const int tl = opaque(t);
@@ -791,11 +734,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       if constexpr (PIPE) {
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s) h[s] = hnext[s];
-      } else if constexpr (RAWPIPE) {
-        const R sa = p.ant_rel[a];
-        const R cs = bm_c<R>(sa * sa);
-#pragma unroll
-        for (int c = 0; c < CHN::kChunks; ++c) CHN::chunk_from_words(c, wnext[c], tl, h, cs);
       } else {
         CHN::template gen<FREL>(p, key, trial, a, tl, rx, h);
       }
@@ -807,13 +745,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       // splits the exchange windows' basic blocks; profiles/r02/ab/ab32_lastant.json).
       // Ablation ABL_RNG: antenna a+1's synthetic channel, in window 0.
       auto hfill = [&](int w) __attribute__((always_inline)) {
-        if constexpr (RAWPIPE) {
-          constexpr int NC = CHN::kChunks, NW = 2 * FFT::XCHG;
-#pragma unroll
-          for (int c = 0; c < NC; ++c)
-            if (c >= w * NC / NW && c < (w + 1) * NC / NW)
-              wnext[c] = CHN::chunk_words(c, key, trial, ST_CHAN, (uint32_t)an, tl, S);
-        }
         if constexpr (PIPE) {
           constexpr int NC = CHN::kChunks, NW = 2 * FFT::XCHG;
           if (MIMO_ABL(p, ABL_RNG)) {
@@ -831,7 +762,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       C he[CSI ? NSLOT : 1];
       if constexpr (CSI) {
         C zc[NSLOT];
-        CHN::normals(key, trial, ST_CSI, (uint32_t)a, tl, S, zc);
+        CHN::normals(key, csi_trial, ST_CSI, (uint32_t)a, tl, S, zc);
         const R sc = p.csi_b * sqrt_ieee(pw_csi[a]);
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s)
@@ -851,13 +782,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         vk = fmar(e2[s], inv_nrm[s] * inv_nrm[s], vk);  // inv_nrm = 0 off band
       }
       if (main_pass) {
-#if MIMO_VK_DPP
         vk = wave_sum_lane63(vk);
         if (lane == 63) vk_part[a & 1][wid] = vk;  // read after the IFFT's first barrier
-#else
-        vk = wave_sum(vk);
-        if (lane == 0) vk_part[a & 1][wid] = vk;
-#endif
       }
       SL::scatter(d, x, t0);
       if (!MIMO_ABL(p, ABL_FFT))
@@ -879,12 +805,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         const R x = fmar(vks, p.inv_vk0, -R(1));
         // Polynomial alpha: -7 % at F = 2048, but +3 % at F = 8192 (SGPR pressure of the
         // 8 waves/team instance, tools/ab_libs.py), so only up to F = 4096.
-        if (MIMO_ALPHA_POLY && sizeof(R) == 4 && F <= 4096 && absr(x) <= p.alpha_xlim) {
+        if (sizeof(R) == 4 && F <= 4096 && absr(x) <= p.alpha_xlim) {
           R acc = p.apoly[8];
 #pragma unroll
           for (int i = 7; i >= 0; --i) acc = fmar(acc, x, p.apoly[i]);
           alpha_a = acc;
-        } else if (MIMO_ALPHA_CHEB64 && sizeof(R) == 8 && absr(x) <= p.alpha_xlim) {
+        } else if (sizeof(R) == 8 && absr(x) <= p.alpha_xlim) {
           // Clenshaw: b_k = c_k + 2 t b_{k+1} - b_{k+2}; alpha = c_0 + t b_1 - b_2
           // (~38 f64 ops instead of the library exp + erfc)
           const double t2 = 2.0 * ((double)x / (double)p.alpha_xlim);

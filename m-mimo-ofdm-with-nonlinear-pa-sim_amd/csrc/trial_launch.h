@@ -13,16 +13,9 @@ constexpr int team_size(int F) { return F >= 1024 ? F / 16 : 64; }
 // F = 8192: 8 points per thread as well (T = 1024, 4 waves/SIMD at 128 VGPRs): its one
 // 136 KiB exchange buffer allows one team per CU either way, and the 16-point team
 // (T = 512, 2 waves/SIMD) measured 3.3 % slower despite fewer spills
-// (profiles/r02/ab/ab8k_f64_team_pipe.json).
-#ifndef MIMO_F64_P16_MAXF
-#define MIMO_F64_P16_MAXF 0  // A/B knob: fp64 instances with 16 points per thread up to this F
-#endif
-#ifndef MIMO_F64_T8192
-#define MIMO_F64_T8192 1024  // fp64 F >= 8192 team size (A/B knob; 1024: 8 points per thread, 4 waves/SIMD, -3.3 % vs 512)
-#endif
-constexpr int team_size64(int F) {
-  return F >= 8192 ? F / (8192 / MIMO_F64_T8192) : (F <= MIMO_F64_P16_MAXF && F >= 1024) ? F / 16 : F >= 512 ? F / 8 : 64;
-}
+// (profiles/r02/ab/ab8k_f64_team_pipe.json); 16 points per thread below F = 8192 measured
+// slower too (profiles/r02/ab/ab64_p16_one_wave.json).
+constexpr int team_size64(int F) { return F >= 512 ? F / 8 : 64; }
 // Alternative team (8 points per thread: half the registers, 2x the waves, one more
 // LDS exchange per transform), selectable with MIMO_TEAM=<T> for A/B measurements.
 constexpr int alt_team_size(int F) { return F >= 1024 ? F / 8 : team_size(F); }

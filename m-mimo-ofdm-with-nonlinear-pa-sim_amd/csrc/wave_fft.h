@@ -31,26 +31,20 @@
 
 namespace mimo {
 
-#ifndef MIMO_WAVE_FFT64
-#define MIMO_WAVE_FFT64 1  // fp64 instances up to F = 4096 (A/B knob)
-#endif
-#ifndef MIMO_WAVE_FFT32
-#define MIMO_WAVE_FFT32 0  // fp32 instances from F = 8192 (8-wave teams): measured +1.2 %, off
-#endif
 
 // The plan needs at least two waves and whole radix-WV butterflies per thread.
 constexpr bool wave_fft_ok(int F, int T) {
   return T >= 128 && T % 64 == 0 && (F / T) >= (T / 64) && (F / T) % (T / 64) == 0;
 }
 // Instances that use it (kernel and engine): fp64 up to F = 4096 (F = 8192's padded rows
-// would not fit the 160 KiB LDS next to the fp64 tables).  fp32 from F = 8192 (8-wave
-// teams) behind MIMO_WAVE_FFT32: interleaved A/B on config 5's array 17.43 -> 17.64 ms
-// (profiles/r02/ab/ab_wavefft_8192_f32.json); below F = 8192 the 2-wave fp32 teams need only
-// two exchanges per transform, which the split would raise to three.
+// would not fit the 160 KiB LDS next to the fp64 tables).  fp32: not used (F = 8192's 8-wave
+// teams measured 17.43 -> 17.64 ms with it, profiles/r02/ab/ab_wavefft_8192_f32.json; below
+// F = 8192 the 2-wave fp32 teams need only two exchanges per transform, which the split
+// would raise to three).
 // fp64 config 2: 58.82 -> 58.50 ms (profiles/r02/ab/ab_wavefft_2048_f64.json).  The
 // barriers were not what the exchanges cost: their LDS round trips remain.
 constexpr bool wave_fft_used(int F, int T, bool f64) {
-  return wave_fft_ok(F, T) && (f64 ? (MIMO_WAVE_FFT64 && F <= 4096) : (MIMO_WAVE_FFT32 && F >= 8192));
+  return wave_fft_ok(F, T) && f64 && F <= 4096;
 }
 constexpr int wave_fft_fw(int F, int T) { return F / (T / 64); }
 constexpr int wave_fft_tw_inter(int F, int T) { return fft_tw_total(wave_fft_fw(F, T), F / T); }

@@ -137,6 +137,30 @@ def acquire_device_slot(dev: int) -> bool:
     return False
 
 
+def wait_for_device_slot(dev: int, still_open, progress, stall_s: float = None, poll_s: float = 0.02) -> bool:
+    """Wait for an engine slot on ``dev`` while the shared counters are open.  Returns False
+    when the counters closed (the slot holders finished the point: nothing left to do), True
+    once a slot is held -- or when the counters made no progress for ``stall_s`` seconds
+    (MIMO_SLOT_STALL_S, default 30): the slots are then held by processes that do not work
+    on these counters, and this worker creates its engine beyond MIMO_MAX_ENGINES_PER_DEVICE
+    rather than wait forever."""
+    stall_s = float(os.environ.get("MIMO_SLOT_STALL_S", "30")) if stall_s is None else stall_s
+    last, t_last = progress(), time.monotonic()
+    while not acquire_device_slot(dev):
+        if not still_open():
+            return False
+        now = progress()
+        if now != last:
+            last, t_last = now, time.monotonic()
+        elif time.monotonic() - t_last > stall_s:
+            import warnings
+            warnings.warn(f"no engine slot on device {dev} and no progress on the shared counters for "
+                          f"{stall_s:.0f} s: creating an engine beyond MIMO_MAX_ENGINES_PER_DEVICE")
+            return True
+        time.sleep(poll_s)
+    return still_open()  # a slot freed because its holder finished the point: maybe done
+
+
 class Link:
     """(mp_model.py:16-87)"""
 
@@ -253,12 +277,14 @@ class Link:
             return bool(np.any((err < self.n_err_min) & (bits < self.bits_sent_max)))
 
         dev = self.device if self.device is not None else _default_device()
-        while not acquire_device_slot(dev):  # the device has its engines: wait, no GPU use
-            if not still_open():
+        if err_np is not None:
+            # Shared counters (the drivers' mp.Array): other workers of this point may own the
+            # device's engines, so wait for a slot while they make progress on the counters.
+            if not wait_for_device_slot(dev, still_open, lambda: (float(np.sum(err_np)),
+                                                                  float(np.sum(n_bits_sent_shared_arr[:])))):
                 return
-            time.sleep(0.02)
-        if not still_open():  # a slot freed because its holder finished the point
-            return
+        else:
+            acquire_device_slot(dev)  # private counters: nobody else closes them, never wait
         eng = self.engine(reroll_chan)
         seed = _seed64(seed_arr)
         iters_all = np.asarray(cnc_n_iter_lst, dtype=np.int64).reshape(-1)
@@ -316,8 +342,11 @@ class Link:
             col = np.concatenate(([0], col))
         seeds = [_seed64(s) for s in seed_arrs]
         trial = np.zeros(P, dtype=np.int64)
-        n_err = np.asarray(n_err)
-        n_bits = np.asarray(n_bits)
+        n_idx = len(col)
+        for name, arr in (("n_err", n_err), ("n_bits", n_bits)):
+            # added to in place: a copy (list, mp.Array, other dtype) would silently drop the totals
+            if not (isinstance(arr, np.ndarray) and arr.dtype == np.float64 and arr.shape == (P, n_idx)):
+                raise TypeError(f"{name} must be a float64 ndarray of shape ({P}, {n_idx}) (added to in place)")
         while True:
             todo = []
             for i in range(P):

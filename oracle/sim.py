@@ -172,6 +172,9 @@ def mcnc_receive(cfg, iters, z, const, p, h_prop, agc_vec, pp, gain):
     return out
 
 
+FIXED_CSI_TRIAL = 0xFFFFFFFF  # CSI stream counter of fixed-channel runs (csrc/trial_kernel.h kFixedCsiTrial)
+
+
 def draws(cfg: SimConfig, seed: int, trials):
     """All random inputs of a batch of trials from the Philox streams."""
     trials = np.asarray(trials, dtype=np.int64)
@@ -180,7 +183,11 @@ def draws(cfg: SimConfig, seed: int, trials):
                z_noise=philox.noise_normals(seed, trials, cfg.n_sc),
                loc_u=philox.loc_uniforms(seed, trials))
     if cfg.csi_eps is not None:
-        out["z_csi"] = philox.csi_normals(seed, trials, cfg.n_sc, cfg.n_ant)
+        # a fixed channel (reroll_chan=False) keeps the one erroneous estimate Link.__init__
+        # drew (mp_model.py:87; set_precoding_and_recalculate_agc is not called in the loop,
+        # :190-206): every trial reads the same, trial-independent CSI draw
+        csi_trials = np.full_like(trials, FIXED_CSI_TRIAL) if cfg.channel == "table" else trials
+        out["z_csi"] = philox.csi_normals(seed, csi_trials, cfg.n_sc, cfg.n_ant)
     return out
 
 

@@ -1,0 +1,49 @@
+"""bench.py's rank launcher: ``--gpus N`` with no outer torchrun starts
+N ranks itself (a torch.distributed.run child process, no exec) and reports n_gpus = N;
+inside the ranks WORLD_SIZE must equal --gpus."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _run(args, env_extra=None, timeout=240):
+    env = dict(os.environ, MIMO_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, env=env,
+                          timeout=timeout, cwd=REPO)
+
+
+def _json_line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_gpus_two_launches_two_ranks_without_outer_torchrun():
+    p = _run(["--gpus", "2", "--no-cpu-baseline", "--check-launch"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _json_line(p.stdout)
+    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2
+
+
+def test_world_size_mismatch_exits_nonzero():
+    p = _run(["--gpus", "2", "--check-launch"], env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_gpus_two_on_one_gpu_reports_both_ranks():
+    """The full bench step with two gloo ranks sharing GPU 0 (the driver's N > 1 path uses RCCL,
+    one GPU per rank): the line reports n_gpus 2 and counts trials of both ranks."""
+    p = _run(["--gpus", "2", "--no-cpu-baseline", "--steps", "2", "--warmup", "1", "--batch", "4096"], timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _json_line(p.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "trial-sharded x2"
+    assert d["value"] > 0 and 0 < d["ber"][0] < 1e-2

@@ -108,7 +108,9 @@ def test_edge_cases_empty_subsets_and_index_limits(prec):
 def test_table_channel_vs_oracle(receiver, csi, prec):
     """MIMO_CH_TABLE (Link.simulate(reroll_chan=False), mp_model.py:190-206): one fixed
     channel matrix for every trial -- exact per-trial counts vs the oracle's fixed-matrix
-    path (parity with the reference unpinned: no fixture captures reroll_chan=False)."""
+    path (parity with the reference unpinned: no fixture captures reroll_chan=False).  With
+    CSI error the erroneous estimate is drawn once and shared by every trial, as the
+    reference keeps the one Link.__init__ drew (mp_model.py:87)."""
     rng = np.random.default_rng(77)
     A, S, F = 8, 256, 512
     h = (rng.standard_normal((A, F)) + 1j * rng.standard_normal((A, F))) * np.sqrt(0.5) * 3e-7
@@ -140,3 +142,20 @@ def test_link_fixed_rayleigh_channel_equals_table_engine():
     ref = sim.run_trials(cfg, _seed64([4, 5, 6]), np.arange(200), iters=[0, 1], incl_clean=True)
     np.testing.assert_array_equal(np.asarray(err[:], np.int64), ref.sum(0))
     assert list(bits[:]) == [1024.0 * 200] * 3
+
+
+def test_table_channel_ignores_rx_offset_and_empty_points_launch_nothing():
+    """A table engine never uses the RX position, so rx_y != rx_x is accepted with a fixed
+    channel (only LoS / two-path need rx_y == rx_x when the RX does not move); a
+    run_points call whose points all have n_trials == 0 launches nothing and adds nothing."""
+    rng = np.random.default_rng(5)
+    A, S, F = 4, 128, 256
+    h = (rng.standard_normal((A, F)) + 1j * rng.standard_normal((A, F))) * 1e-7
+    cfg = sim.SimConfig(A, S, F, 16, ibo_db=1.0, snr_db=14.0, channel="table", table_h=h,
+                        rx_pos=(212.0, 100.0, 1.5))
+    eng = engine_for(cfg)
+    _, _, per = eng.run(8, 0, 16, [0, 1], False, per_trial=True)
+    assert_counts_equal(per, sim.run_trials(cfg, 8, np.arange(16), iters=[0, 1]), "table rx_y != rx_x")
+    pt = dict(eng.point_kw)
+    e, b, per0 = eng.run_points([pt, pt], [1, 2], [0, 5], [0, 0], [0, 1], False, per_trial=True)
+    assert e.sum() == 0 and b.sum() == 0 and per0.shape == (0, 2)

@@ -199,6 +199,53 @@ def test_waiting_worker_returns_when_point_is_done(tmp_path, monkeypatch):
     link.simulate(False, True, np.array([0, 1]), [1], err, bits)
 
 
+def test_private_counters_never_wait_for_a_slot(tmp_path, monkeypatch):
+    """a caller with private counters (not an mp.Array) does not wait for a slot
+    (nobody else would close its counters): it goes straight to the engine."""
+    import mp_model
+    monkeypatch.setenv("MIMO_LOCK_DIR", str(tmp_path))
+    monkeypatch.setattr(mp_model, "acquire_device_slot", lambda dev: False)
+    link, _ = build_link(bits_sent_max=1000, n_err_min=10, device=0)
+    called = []
+
+    def fake_engine(reroll=True):
+        called.append(reroll)
+        raise RuntimeError("engine reached")
+    monkeypatch.setattr(link, "engine", fake_engine)
+    with pytest.raises(RuntimeError, match="engine reached"):
+        link.simulate(False, True, np.array([0, 1]), [1], np.zeros(2), np.zeros(2))
+    assert called == [True]
+
+
+def test_slot_wait_is_bounded_when_counters_stall(tmp_path, monkeypatch):
+    """Shared counters that make no progress while every slot is held by other processes:
+    the worker stops waiting after the stall time and creates its engine anyway."""
+    import mp_model
+    monkeypatch.setattr(mp_model, "acquire_device_slot", lambda dev: False)
+    with pytest.warns(UserWarning, match="MIMO_MAX_ENGINES_PER_DEVICE"):
+        assert mp_model.wait_for_device_slot(0, lambda: True, lambda: (0.0, 0.0), stall_s=0.1)
+    # counters that close while waiting: False (nothing left to do)
+    state = {"n": 0}
+
+    def still_open():
+        state["n"] += 1
+        return state["n"] < 5
+    assert not mp_model.wait_for_device_slot(0, still_open, lambda: state["n"], stall_s=60)
+
+
+def test_simulate_points_rejects_counters_it_cannot_add_into(monkeypatch):
+    """simulate_points adds into n_err / n_bits in place; a list or another dtype
+    would be copied and the totals lost, so it raises instead."""
+    link, _ = build_link(bits_sent_max=1000, n_err_min=10, device=0)
+    link.set_snr(10.0)
+    monkeypatch.setattr(link, "engine", lambda reroll=True: object())
+    pp = [link.point_params()]
+    with pytest.raises(TypeError, match="float64 ndarray"):
+        link.simulate_points(False, True, [0, 1], [[1]], pp, [[0.0, 0.0]], np.zeros((1, 2)))
+    with pytest.raises(TypeError, match="float64 ndarray"):
+        link.simulate_points(False, True, [0, 1], [[1]], pp, np.zeros((1, 2)), np.zeros((1, 3)))
+
+
 def test_multi_user_is_rejected_explicitly():
     """Multi-user OFDM / MU-MR / MU-ZF (modulation.py:363-382, antenna_array.py:188-305) are
     not part of this build: they raise instead of running unverified code."""
