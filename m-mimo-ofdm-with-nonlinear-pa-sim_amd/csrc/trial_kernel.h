@@ -256,8 +256,43 @@ __device__ __forceinline__ C pa_apply(int kind, C x, R sat, R sqrt_sat, R inv_sa
   return mkc(x.x * sc, x.y * sc);
 }
 
-// Rapp with an integer hardness: (pw/sat)^p by multiplication (config 5 uses p = 3),
-// one log + one exp per sample instead of two of each.
+// y^(-1/N) for y >= 1 (the Rapp gain at integer hardness, N = 2p).  fp32: hardware
+// log / exp.  fp64: the fp32 hardware value as the seed (~2^-22) and two Newton steps
+// z <- z + (z / N)(1 - y z^N) (quadratic: 2^-42, then below the fp64 rounding), 12 f64
+// ops + 2 fp32 transcendentals instead of the library log2 + exp2 (~60 instructions).
+template <int N>
+__device__ __forceinline__ float rpow_neg_inv(float y) {
+  return __builtin_amdgcn_exp2f((-1.0f / N) * __builtin_amdgcn_logf(y));
+}
+template <int N>
+__device__ __forceinline__ double rpow_neg_inv(double y) {
+  double z = (double)rpow_neg_inv<N>((float)y);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    double zn = z;  // z^N by repeated squaring (N = 4, 6 in practice)
+    {
+      double b = z, acc = 1.0;
+      int n = N;
+      bool first = true;
+#pragma unroll
+      for (int k = 0; k < 8 && n; ++k) {
+        if (n & 1) {
+          acc = first ? b : acc * b;
+          first = false;
+        }
+        n >>= 1;
+        if (n) b *= b;
+      }
+      zn = acc;
+    }
+    const double e = fma(-y, zn, 1.0);
+    z = fma(z * (1.0 / N), e, z);
+  }
+  return z;
+}
+
+// Rapp with an integer hardness: (pw/sat)^p by multiplication (config 5 uses p = 3), then
+// (1 + (pw/sat)^p)^(-1/(2p)) by rpow_neg_inv.
 template <int IP, int P, class C, typename R = real_of<C>>
 __device__ __forceinline__ void rapp_int(C (&d)[P], R inv_sat) {
 #pragma unroll
@@ -266,7 +301,7 @@ __device__ __forceinline__ void rapp_int(C (&d)[P], R inv_sat) {
     R up = u;
 #pragma unroll
     for (int i = 1; i < IP; ++i) up *= u;
-    const R sc = exp2_r((R(-0.5) / IP) * log2_r(R(1) + up));
+    const R sc = rpow_neg_inv<2 * IP>(R(1) + up);
     d[m] = mkc(d[m].x * sc, d[m].y * sc);
   }
 }

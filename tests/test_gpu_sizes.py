@@ -55,3 +55,28 @@ def test_sizes_vs_oracle(monkeypatch, F, S, A, M, pa, p, ibo, team, prec):
     assert_counts_equal(per, ref, f"{F}/{S}/{A}/{M}/{pa}/{p}/{ibo}/{team} {prec}")
     np.testing.assert_array_equal(err, per.sum(0))
     assert all(int(b) == len(trials) * S * int(np.log2(M)) for b in bits)
+
+
+CONFIG5 = [
+    # A,  M,  pa,        p,   ibo, channel,    receiver, trials
+    (256, 64, "rapp", 3.0, 3.0, "rayleigh", "cnc", 6),    # config-5 array geometry (one user)
+    (8, 16, "softlim", 0.0, 1.0, "rayleigh", "mcnc", 8),  # MCNC array passes through the F 8192 path
+    (16, 16, "softlim", 0.0, 2.0, "los", "cnc", 8),       # closed-form LoS on the F 8192 path
+]
+
+
+@pytest.mark.parametrize("prec", PRECISIONS)
+@pytest.mark.parametrize("A,M,pa,p,ibo,channel,receiver,n", CONFIG5)
+def test_config5_array_vs_oracle(A, M, pa, p, ibo, channel, receiver, n, prec):
+    """BASELINE config 5's array at one user (256 antennas, F 8192, 4096 sub-carriers,
+    Rapp p = 3) and the other F 8192 receivers / channels: per-trial counts EXACTLY equal to
+    the oracle's (the fp64 instance runs the pair-wave FFT and block state memory)."""
+    F, S = 8192, 4096
+    snr = float(sim.rm.ebn0_to_snr(15.0, S, S, M))
+    cfg = sim.SimConfig(A, S, F, M, pa=pa, p_hardness=p, ibo_db=ibo, snr_db=snr, channel=channel, receiver=receiver)
+    iters = [0, 1, 2]
+    ref = sim.run_trials(cfg, 77, np.arange(n), iters=iters, incl_clean=True, chunk=2)
+    eng = engine_for(cfg, precision=prec)
+    _, _, per = eng.run(77, 0, n, iters, True, per_trial=True)
+    print("config5", A, M, pa, channel, receiver, eng.describe(), per.sum(0), ref.sum(0))
+    assert_counts_equal(per, ref, f"config5 {A}/{M}/{pa}/{channel}/{receiver} {prec}")
