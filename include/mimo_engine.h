@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MIMO_ABI_VERSION 4
+#define MIMO_ABI_VERSION 5
 
 enum { MIMO_OK = 0, MIMO_EINVAL = -1, MIMO_EHIP = -2, MIMO_ENOKERNEL = -3, MIMO_ENOMEM = -4 };
 enum { MIMO_PA_NONE = 0, MIMO_PA_SOFTLIM = 1, MIMO_PA_RAPP = 2, MIMO_PA_TOI = 3 };
@@ -69,6 +69,12 @@ typedef struct mimo_config {
   const double* chan_table; /* MIMO_CH_TABLE only: [n_ant][n_fft] complex channel matrix
                                (Miso*Fd.channel_mat_fd), the same for every trial -- what
                                Link.simulate(reroll_chan=False) uses (mp_model.py:190-206) */
+  int32_t chan_replay_period; /* 0 (default): an independent Rayleigh channel per trial.
+                               > 0 (diagnostic, Rayleigh only): trial i draws the channel of
+                               trial i mod period, emulating the reference's workers that all
+                               replay one seeded channel sequence (channel.py:209-212);
+                               bits and noise stay per trial.  Used to size the published
+                               curves' channel variance (tests/test_gpu_link.py).  (ABI 5) */
 } mimo_config;
 
 /* Grid-point parameters: what Link keeps in its PA / receiver / noise objects. */

@@ -40,7 +40,7 @@ class MimoConfig(ctypes.Structure):
                 ("constel_size", ctypes.c_int32), ("cp_len", ctypes.c_int32), ("channel_kind", ctypes.c_int32),
                 ("receiver_kind", ctypes.c_int32), ("device", ctypes.c_int32), ("rx_pos", ctypes.c_double * 3),
                 ("rx_loc_var", ctypes.c_double), ("reroll_chan", ctypes.c_int32), ("precision", ctypes.c_int32),
-                ("tx_pos", _dp), ("carrier_freqs", _dp), ("chan_table", _dp)]
+                ("tx_pos", _dp), ("carrier_freqs", _dp), ("chan_table", _dp), ("chan_replay_period", ctypes.c_int32)]
 
 
 class MimoPoint(ctypes.Structure):
@@ -126,7 +126,8 @@ class Engine:
     """One configured system (the deep-copied objects of a ``Link``) on one GPU."""
 
     def __init__(self, n_ant, n_sub_carr, n_fft, constel_size, cp_len, channel, receiver, tx_pos, rx_pos,
-                 rx_loc_var, carrier_freqs, reroll=True, device=-1, precision=None, chan_table=None):
+                 rx_loc_var, carrier_freqs, reroll=True, device=-1, precision=None, chan_table=None,
+                 chan_replay_period=0):
         L = lib()
         self.precision = precision or default_precision()
         if self.precision not in PRECISIONS:
@@ -146,7 +147,8 @@ class Engine:
                          rx_loc_var=float(rx_loc_var), reroll_chan=int(bool(reroll)),
                          precision=PRECISIONS[self.precision],
                          tx_pos=_ptr(self._tx, ctypes.c_double), carrier_freqs=_ptr(self._fr, ctypes.c_double),
-                         chan_table=_ptr(self._tab, ctypes.c_double) if self._tab is not None else None)
+                         chan_table=_ptr(self._tab, ctypes.c_double) if self._tab is not None else None,
+                         chan_replay_period=int(chan_replay_period))
         cfg.rx_pos[:] = [float(v) for v in rx_pos]
         h = L.mimo_engine_create(ctypes.byref(cfg))
         if not h:

@@ -115,25 +115,20 @@ AlphaFit fit_alpha(double g0sq) {
   return p;
 }
 
-// fp64 Box-Muller tables (real.h ln_lut / sincos_lut), computed in long double.
+// fp64 Box-Muller tables (real.h ln_unit / sincos_lut), computed in long double.
 std::vector<double2> lut64_table() {
   std::vector<double2> t(mimo::kLut64);
-  for (int i = 0; i < mimo::kLnTab; ++i) {
-    // bucket i: high word 0x3FE00000 | (i & 255) << 12 (i < 256) or 0x3FF00000 | ... (i >= 256)
-    const bool one = i >= 256;
-    const int j = i & 255;
-    const long double lo = one ? 1.0L + j / 256.0L : 0.5L + j / 512.0L;
-    const long double w = one ? 1.0L / 256 : 1.0L / 512;
-    double c;
-    if ((one && j == 0) || (!one && j == 255)) {
-      c = 1.0;  // the buckets next to 1: t = m - 1 exactly
-    } else {
-      const long double ctr = lo + 0.5L * w;
-      int ex;
-      const long double fr = std::frexp(1.0L / ctr, &ex);       // [0.5, 1)
-      c = (double)std::ldexp(std::round(std::ldexp(fr, 12)), ex - 12);  // 12 significant bits
+  {  // real.h ln_unit: bucket i = m in [0.5 + i 2^-10, 0.5 + (i + 1) 2^-10), c = 1 for the top one
+    for (int i = 0; i < mimo::kLnTab; ++i) {
+      double c = 1.0;
+      if (i != mimo::kLnTab - 1) {
+        const long double ctr = 0.5L + (i + 0.5L) / 1024.0L;
+        int ex;
+        const long double fr = std::frexp(1.0L / ctr, &ex);
+        c = (double)std::ldexp(std::round(std::ldexp(fr, 12)), ex - 12);
+      }
+      t[i] = make_double2(c, (double)(-std::log((long double)c)));
     }
-    t[i] = make_double2(c, (double)(-std::log((long double)c)));
   }
   for (int i = 0; i < mimo::kScTab; ++i) {
     const long double a = 2.0L * 3.14159265358979323846264338327950288L * i / mimo::kScTab;
@@ -280,6 +275,9 @@ int validate_config(const mimo_config* c) {
   if (!c->tx_pos) return fail(MIMO_EINVAL, "tx_pos is required");
   if (c->precision != MIMO_PREC_F64 && c->precision != MIMO_PREC_F32)
     return fail(MIMO_EINVAL, "precision must be MIMO_PREC_F64 or MIMO_PREC_F32");
+  if (c->chan_replay_period < 0) return fail(MIMO_EINVAL, "chan_replay_period must be >= 0");
+  if (c->chan_replay_period > 0 && c->channel_kind != MIMO_CH_RAYLEIGH)
+    return fail(MIMO_EINVAL, "chan_replay_period applies to the Rayleigh channel only");
   return MIMO_OK;
 }
 
@@ -634,6 +632,7 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
     if (const char* env = std::getenv("MIMO_ABLATE")) base.ablate = (uint32_t)std::strtoul(env, nullptr, 0);
 #endif
     base.counts = e->d_counts;
+    base.chan_period = (uint32_t)std::max(0, c.chan_replay_period);
     // per-point parameter table (host), built once
     std::vector<TP> ptab(n_points, base);
     for (int i = 0; i < n_points; ++i) fill_point(e, pts[i], seeds[i], 0, ptab[i]);

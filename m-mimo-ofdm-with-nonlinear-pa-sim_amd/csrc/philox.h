@@ -74,11 +74,11 @@ __device__ __forceinline__ double bm_c<double>(double scale2) {
 __device__ __forceinline__ float bm_log(uint32_t w0, float) {
   return __builtin_amdgcn_logf(fmaf((float)w0, 2.3283064365386963e-10f, 1.1641532182693481e-10f));
 }
-// fp64: LDS-table ln (real.h ln_lut; the trial kernel loads lut64 first).  The series
+// fp64: LDS-table ln (real.h ln_unit; the trial kernel loads lut64 first).  The series
 // forms (ln_pos, sincos_rev) measured 1.4-3.9 % slower.
 __device__ __forceinline__ double bm_log(uint32_t w0, double) {
   const double u1 = ((double)w0 + 0.5) * 2.3283064365386963e-10;  // exact argument
-  return ln_lut(u1);
+  return ln_unit(u1);
 }
 
 __device__ __forceinline__ float2 box_muller(uint32_t w0, uint32_t w1, float c = kNegLn2) {
@@ -91,7 +91,7 @@ __device__ __forceinline__ float2 box_muller(uint32_t w0, uint32_t w1, float c =
   return make_float2(rho * __builtin_amdgcn_cosf(u2), rho * __builtin_amdgcn_sinf(u2));
 }
 __device__ __forceinline__ double2 box_muller(uint32_t w0, uint32_t w1, double c) {
-  const double rho = sqrt_nr(c * bm_log(w0, 0.0));  // argument > 0: u1 < 1 always
+  const double rho = sqrt_n1(c * bm_log(w0, 0.0));  // argument > 0: u1 < 1 always
   double s, co;
   sincos_lut(w1, s, co);  // revolutions w1 2^-32, from the word itself
   return make_double2(rho * co, rho * s);

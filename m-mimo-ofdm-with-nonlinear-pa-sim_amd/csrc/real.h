@@ -83,36 +83,11 @@ __device__ __forceinline__ double rcp_r(double x) { return 1.0 / x; }
 // (ln: ~13 f64 ops instead of ~25 plus a Newton reciprocal for the atanh series; sincos:
 // ~15 instead of ~35 for a quadrant Taylor series; the series forms are in git history).
 // Table (host-built, engine.hip lut64_table, loaded into LDS at kernel start):
-//   [0, 512):   (c_i, -ln c_i) for m in bucket i of [sqrt(1/2), sqrt(2)) (i = bit 20..12 of
-//               the high word of m: exponent LSB + 8 mantissa bits); c_i ~ 1/centre_i rounded
-//               to 12 bits, c_i = 1 for the two buckets around 1 (relative accuracy at x -> 1)
+//   [0, 512):   (c_i, -ln c_i) for m in bucket i of [0.5, 1) (ln_unit: the top 9 mantissa
+//               bits); c_i ~ 1/centre_i rounded to 12 bits, c_i = 1 for the top bucket
 //   [512, 768): (cos, sin)(2 pi i / 256)
 constexpr int kLnTab = 512, kScTab = 256, kLut64 = kLnTab + kScTab;
 static __shared__ double2 lut64[kLut64];
-
-// ln x for a positive normal double: x = m 2^e, m in [sqrt(1/2), sqrt(2)); t = m c_i - 1
-// (|t| <= 2^-8), ln x = e ln 2 - ln c_i + log1p(t) with the series to t^7.  <= ~1.5 ulp.
-__device__ __forceinline__ double ln_lut(double x) {
-  const uint32_t hi = (uint32_t)__double2hiint(x), lo = (uint32_t)__double2loint(x);
-  const uint32_t man = hi & 0xFFFFFu;
-  const bool big = man >= 0x6A09Eu;  // m = 1.man >= sqrt(2): take the [0.5, 1) binade
-  const int e = (int)(hi >> 20) - 1023 + (big ? 1 : 0);
-  const uint32_t mhi = man | (big ? 0x3FE00000u : 0x3FF00000u);
-  const double m = __hiloint2double((int)mhi, (int)lo);
-  const double2 cl = lut64[(mhi >> 12) & 511u];
-  const double t = fma(m, cl.x, -1.0);
-  double q = 1.0 / 7;
-  q = fma(q, t, -1.0 / 6);
-  q = fma(q, t, 1.0 / 5);
-  q = fma(q, t, -1.0 / 4);
-  q = fma(q, t, 1.0 / 3);
-  q = fma(q, t, -0.5);
-  const double p = fma(t * t, q, t);
-  constexpr double kLn2Hi = 6.93147180369123816490e-01;  // ln 2 with 21 trailing zero bits
-  constexpr double kLn2Lo = 1.90821492927058770002e-10;
-  const double de = (double)e;
-  return fma(de, kLn2Hi, cl.y) + fma(de, kLn2Lo, p);
-}
 
 // sin / cos of 2 pi w 2^-32 (w: a uint32 word, revolutions): i = nearest 256th,
 // phi = 2 pi (w - i 2^24) 2^-32 in [-pi/256, pi/256], series to phi^7 / phi^6 and the
@@ -151,18 +126,39 @@ __device__ __forceinline__ void sincos_rev_lut(double r, double& sn, double& cs)
   cs = fma(cst.x, c, -(cst.y * s));
 }
 
-// sqrt of a positive normal double (no denormal / overflow scaling): v_rsq_f64 seed and
-// the Goldschmidt / Newton refinement of the compiler's lowering.
-__device__ __forceinline__ double sqrt_nr(double x) {
+// ln u for u in (0, 1) (the Box-Muller radius argument): u = m 2^e with m in [0.5, 1) and
+// e <= 0, so e ln 2 and ln m have the same sign and need no range fold; bucket i of m
+// (the top 9 mantissa bits, width 2^-10) gives c_i ~ 1 / centre_i (12 bits; c = 1 for the
+// top bucket: t = m - 1 exactly as u -> 1), t = m c_i - 1 with |t| < 2^-10, and
+// log1p(t) to t^6 (truncation < 2^-60 relative).
+__device__ __forceinline__ double ln_unit(double x) {
+  const uint32_t hi = (uint32_t)__double2hiint(x), lo = (uint32_t)__double2loint(x);
+  const int e = (int)(hi >> 20) - 1022;
+  const double m = __hiloint2double((int)((hi & 0xFFFFFu) | 0x3FE00000u), (int)lo);
+  const double2 cl = lut64[(hi >> 11) & 511u];
+  const double t = fma(m, cl.x, -1.0);
+  double q = -1.0 / 6;
+  q = fma(q, t, 1.0 / 5);
+  q = fma(q, t, -1.0 / 4);
+  q = fma(q, t, 1.0 / 3);
+  q = fma(q, t, -0.5);
+  const double p = fma(t * t, q, t);
+  constexpr double kLn2Hi = 6.93147180369123816490e-01;
+  constexpr double kLn2Lo = 1.90821492927058770002e-10;
+  const double de = (double)e;
+  return fma(de, kLn2Hi, cl.y) + fma(de, kLn2Lo, p);
+}
+// sqrt of a positive normal double by the v_rsq_f64 seed (~2^-25) and one Newton step
+// (~2^-49 relative).
+__device__ __forceinline__ double sqrt_n1(double x) {
   const double r = __builtin_amdgcn_rsq(x);
-  double g = x * r, h = 0.5 * r;
-  const double e = fma(-h, g, 0.5);
-  g = fma(g, e, g);
-  h = fma(h, e, h);
-  double d = fma(-g, g, x);
-  g = fma(d, h, g);
-  d = fma(-g, g, x);
-  return fma(d, h, g);
+  const double g = x * r, h = 0.5 * r;
+  return fma(g, fma(-g, h, 0.5), g);
+}
+// 1/sqrt(x), x > 0 finite: seed and one Newton step (~2^-49 relative).
+__device__ __forceinline__ double rsq_n1(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  return fma(y, fma(-0.5 * x * y, y, 0.5), y);
 }
 
 __device__ __forceinline__ float sin_rev(float r) { return __builtin_amdgcn_sinf(r); }

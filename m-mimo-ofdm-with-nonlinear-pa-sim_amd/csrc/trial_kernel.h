@@ -92,6 +92,7 @@ struct TrialParams {
   const TrialParams* points;     // [n_points] (device)
   const uint32_t* point_start;   // [n_points + 1] block offsets (device)
   int n_points;
+  uint32_t chan_period;          // 0, or the channel-replay period (mimo_config.chan_replay_period)
 };
 
 // Ablation switches for cost breakdowns.  Compiled in only with -DMIMO_ABLATION
@@ -244,7 +245,7 @@ __device__ __forceinline__ C pa_apply(int kind, C x, R sat, R sqrt_sat, R inv_sa
   R sc = R(1);
   if (kind == PA_SOFTLIM) {
     if constexpr (sizeof(R) == 4) sc = minr(1.0f, sqrt_sat * rsq_r(pw));
-    else sc = pw > sat ? sqrt_sat * rsq_r(pw) : R(1);
+    else sc = pw > sat ? sqrt_sat * rsq_n1(pw) : R(1);
   } else if (kind == PA_RAPP) {
     // 1 / (1 + (pw/sat)^p)^(1/(2p))
     const R u = pw * inv_sat;
@@ -610,9 +611,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // reference draws the erroneous estimate once (Link.__init__, mp_model.py:87) and keeps
   // it for every trial, so all trials share one draw (trial-independent counter).
   const uint32_t csi_trial = CH == CH_TABLE ? kFixedCsiTrial : trial;
+  // Channel counter: the trial, or (diagnostic, chan_period > 0) the trial modulo the
+  // period -- every group of chan_period trials replays one sequence of Rayleigh channels,
+  // as the reference's forked workers all replay the channel object's seeded generator
+  // (channel.py:209-212, mp_model.py:61); bits and noise stay per trial.
+  const uint32_t ch_trial = p0.chan_period ? trial % p0.chan_period : trial;
   const int S = p.n_sc, A = p.n_ant, L = p.qam_l, hb = p.half_bits;
   const R inv_sqrt_f = p.inv_sqrt_f;
-  if constexpr (sizeof(R) == 8) {  // Box-Muller tables (real.h ln_lut / sincos_lut) into LDS
+  if constexpr (sizeof(R) == 8) {  // Box-Muller tables (real.h ln_unit / sincos_lut) into LDS
     for (int i = t; i < kLut64; i += T) lut64[i] = p.lut[i];
     __syncthreads();
   }
@@ -664,14 +670,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     if constexpr (CH == CH_RAYLEIGH && !CSI) {
       if (!MIMO_ABL(p, ABL_RNG)) {
         R e2[NSLOT];
-        CHN::power(p, key, trial, a, tl, e2);
+        CHN::power(p, key, ch_trial, a, tl, e2);
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s) nrm2[s] += e2[s];
         continue;
       }
     }
     C h[NSLOT];
-    CHN::template gen<FREL>(p, key, trial, a, tl, rx, h);
+    CHN::template gen<FREL>(p, key, ch_trial, a, tl, rx, h);
     if constexpr (CSI) {
       // mp_model.py:264-282: Hhat = sqrt(1-eps^2) H + eps sqrt(mean_k |H|^2) z
       R pw = R(0);
@@ -760,8 +766,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     C hnext[PIPE ? NSLOT : 1];
     if constexpr (PIPE) {
       const R sa = p.ant_rel[0];
-      if (MIMO_ABL(p, ABL_RNG)) CHN::template gen<FREL>(p, key, trial, 0, t, rx, hnext);
-      else CHN::normals(key, trial, ST_CHAN, 0u, t, S, hnext, bm_c<R>(sa * sa));
+      if (MIMO_ABL(p, ABL_RNG)) CHN::template gen<FREL>(p, key, ch_trial, 0, t, rx, hnext);
+      else CHN::normals(key, ch_trial, ST_CHAN, 0u, t, S, hnext, bm_c<R>(sa * sa));
     }
     for (int a = 0; a < A; ++a) {
       const int tl = opaque(t);
@@ -770,7 +776,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s) h[s] = hnext[s];
       } else {
-        CHN::template gen<FREL>(p, key, trial, a, tl, rx, h);
+        CHN::template gen<FREL>(p, key, ch_trial, a, tl, rx, h);
       }
       const int an = a + 1 < A ? a + 1 : a;
       const R san = PIPE ? p.ant_rel[an] : R(0);
@@ -783,12 +789,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         if constexpr (PIPE) {
           constexpr int NC = CHN::kChunks, NW = 2 * FFT::XCHG;
           if (MIMO_ABL(p, ABL_RNG)) {
-            if (w == 0) CHN::template gen<FREL>(p, key, trial, an, tl, rx, hnext);
+            if (w == 0) CHN::template gen<FREL>(p, key, ch_trial, an, tl, rx, hnext);
           } else {
 #pragma unroll
             for (int c = 0; c < NC; ++c)
               if (c >= w * NC / NW && c < (w + 1) * NC / NW)
-                CHN::normals_chunk(c, key, trial, ST_CHAN, (uint32_t)an, tl, S, hnext, bm_c<R>(san * san));
+                CHN::normals_chunk(c, key, ch_trial, ST_CHAN, (uint32_t)an, tl, S, hnext, bm_c<R>(san * san));
           }
         }
       };

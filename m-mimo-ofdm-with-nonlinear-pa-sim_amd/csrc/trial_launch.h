@@ -15,7 +15,10 @@ constexpr int team_size(int F) { return F >= 1024 ? F / 16 : 64; }
 // (T = 512, 2 waves/SIMD) measured 3.3 % slower despite fewer spills
 // (profiles/r02/ab/ab8k_f64_team_pipe.json); 16 points per thread below F = 8192 measured
 // slower too (profiles/r02/ab/ab64_p16_one_wave.json).
-constexpr int team_size64(int F) { return F >= 512 ? F / 8 : 64; }
+#ifndef MIMO_X_P8K
+#define MIMO_X_P8K 8  // temporary A/B knob
+#endif
+constexpr int team_size64(int F) { return F >= 8192 ? F / MIMO_X_P8K : F >= 512 ? F / 8 : 64; }
 // Alternative team (8 points per thread: half the registers, 2x the waves, one more
 // LDS exchange per transform), selectable with MIMO_TEAM=<T> for A/B measurements.
 constexpr int alt_team_size(int F) { return F >= 1024 ? F / 8 : team_size(F); }

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     lib = _engine.lib()
     missing = [n for n in declared_functions() if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.mimo_abi_version() == 4
+    assert lib.mimo_abi_version() == 5
 
 
 def _cfg(**kw):
@@ -55,6 +55,8 @@ def _cfg(**kw):
     (dict(channel_kind=7), "unknown channel_kind"),
     (dict(receiver_kind=0), "unknown receiver_kind"),
     (dict(precision=2), "precision must be"),
+    (dict(chan_replay_period=-1), "chan_replay_period must be >= 0"),
+    (dict(chan_replay_period=8, channel_kind=2), "Rayleigh channel only"),
 ])
 def test_create_rejects_invalid_configs(kw, msg):
     lib = _engine.lib()

@@ -39,3 +39,17 @@ def test_fixed_ber_grid_vs_published(receiver, channel):
     assert out["p95_abs_z"] <= 5.0 and out["max_abs_z"] <= 12.0
     r = out["req_ebn0_at_ber_1e2"]
     assert r["finite_mismatch"] == 0 and r["compared"] >= 70 and r["mean_abs_db"] <= 0.1
+
+
+def test_fixed_ber_grid_baseline_extent():
+    """BASELINE config 4 at its stated extent (Eb/N0 0..30 x IBO 0..7 dB, 0.5 dB steps =
+    915 points, CNC 0..8) on one GPU: every counter of every point closed
+    by the stopping rule, the standard receiver's BER non-increasing in Eb/N0 at every IBO,
+    and the sub-grid shared with the published grid in line with it."""
+    import fixed_ber_check
+    out, ber = fixed_ber_check.run_baseline("rayleigh", "cnc", "f64")
+    print(out)
+    assert out["points"] == 915 and out["all_counters_closed"]
+    assert out["standard_rx_ber_rises"] == 0
+    sh = out["shared_with_published"]
+    assert sh["points"] == 375 and sh["compared"] > 1000 and sh["median_rel"] <= 0.02
