@@ -340,7 +340,8 @@ struct TeamFft {
   // Measured -1.1 % (F 2048), -1.5 % (F 4096), +0.9 % (F 8192: more stages held live);
   // fp64: -2.4 % at F = 2048 (with the channel pipeline off), +1.5 % at F = 4096
   // (profiles/r02/ab/ab64_*.json).
-  static constexpr bool PREFETCH = F <= 4096 && (sizeof(Re) == 4 || F <= 2048);
+  // fp64 F 8192 (16 points per thread): -2.2 % (profiles/r03/ab8k/ab_diet_prefetch.json).
+  static constexpr bool PREFETCH = (F <= 4096 && (sizeof(Re) == 4 || F <= 2048)) || (sizeof(Re) == 8 && F >= 8192);
   // Base holds w(2^k) for k < kMaxB; a stage reads k < bits(S) <= LOG_P.
   static_assert(!PREFETCH || LOG_P <= kMaxB, "Base too small for the plan's largest radix");
   struct Base {

@@ -37,7 +37,7 @@ struct Profile {
 };
 constexpr Profile profile_for(int T, bool aligned, int ch) {
   const int P = kF / T;
-  if (kF64 && kF >= 8192) return Profile{2, 1, false};  // 136 KiB exchange buffer: one team per CU (T = 1024: 4 waves/SIMD)
+  if (kF64 && kF >= 8192) return Profile{2, 1, false};  // 136 KiB exchange buffer: one team per CU (T = 512: 2 waves/SIMD)
   if (kF64) return Profile{2, 1, true};
   if (!aligned) return Profile{2, kF >= 4096 ? 1 : 2, true};  // one buffer from F = 4096: 2 teams/CU
   if (P < 16) return Profile{4, 2, false};

@@ -258,38 +258,23 @@ __device__ __forceinline__ C pa_apply(int kind, C x, R sat, R sqrt_sat, R inv_sa
 }
 
 // y^(-1/N) for y >= 1 (the Rapp gain at integer hardness, N = 2p).  fp32: hardware
-// log / exp.  fp64: the fp32 hardware value as the seed (~2^-22) and two Newton steps
-// z <- z + (z / N)(1 - y z^N) (quadratic: 2^-42, then below the fp64 rounding), 12 f64
-// ops + 2 fp32 transcendentals instead of the library log2 + exp2 (~60 instructions).
+// log / exp.  fp64: the fp32 hardware value z as the seed (~2^-22) and one third-order
+// step z (1 - e)^(-1/N) ~ z (1 + e/N + (N+1) e^2 / (2 N^2)), e = 1 - y z^N (error
+// ~2^-60, below the fp64 rounding): 7 f64 ops + 2 fp32 transcendentals instead of the
+// library log2 + exp2 (~60 instructions).
 template <int N>
 __device__ __forceinline__ float rpow_neg_inv(float y) {
   return __builtin_amdgcn_exp2f((-1.0f / N) * __builtin_amdgcn_logf(y));
 }
 template <int N>
 __device__ __forceinline__ double rpow_neg_inv(double y) {
-  double z = (double)rpow_neg_inv<N>((float)y);
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    double zn = z;  // z^N by repeated squaring (N = 4, 6 in practice)
-    {
-      double b = z, acc = 1.0;
-      int n = N;
-      bool first = true;
-#pragma unroll
-      for (int k = 0; k < 8 && n; ++k) {
-        if (n & 1) {
-          acc = first ? b : acc * b;
-          first = false;
-        }
-        n >>= 1;
-        if (n) b *= b;
-      }
-      zn = acc;
-    }
-    const double e = fma(-y, zn, 1.0);
-    z = fma(z * (1.0 / N), e, z);
-  }
-  return z;
+  static_assert(N == 4 || N == 6, "integer Rapp hardness 2 or 3");
+  const double z = (double)rpow_neg_inv<N>((float)y);
+  const double z2 = z * z;
+  const double zn = N == 4 ? z2 * z2 : z2 * z2 * z2;
+  const double e = fma(-y, zn, 1.0);
+  const double c = e * fma(e, (N + 1.0) / (2.0 * N * N), 1.0 / N);
+  return fma(z, c, z);
 }
 
 // Rapp with an integer hardness: (pw/sat)^p by multiplication (config 5 uses p = 3), then
@@ -726,8 +711,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // in fp64); the opaque copies stop the compiler from hoisting it back out of the loop.
   // Register diet of the fp64 F = 8192 instance (-2.1 %; at F 2048 the |Hhat|^2 half measured
   // +0.8 %): symbols rebuilt from the labels per antenna, |Hhat|^2 recomputed after the FFT.
-  constexpr bool SYMW_RE = !SYMW_LDS && sizeof(R) == 8 && F >= 8192;
-  constexpr bool E2_RE = sizeof(R) == 8 && F >= 8192;
+  constexpr bool SYMW_RE = !SYMW_LDS && sizeof(R) == 8 && F >= 8192;  // off: +13 % at F 8192
+  constexpr bool E2_RE = sizeof(R) == 8 && F >= 8192;                  // off: +2.8 % (ab_diet_prefetch.json)
   C symw_r[SYMW_LDS || SYMW_RE ? 1 : NSLOT];
   uint32_t slab_r[SYMW_RE ? NSLOT : 1];
   auto set_symbols = [&](const uint32_t (&lab_in)[NSLOT]) __attribute__((always_inline)) {

@@ -9,16 +9,13 @@ namespace mimo {
 // Team (workgroup) size per FFT size: 16 points per thread from F = 1024 up, one wave below.
 constexpr int team_size(int F) { return F >= 1024 ? F / 16 : 64; }
 // fp64 instances: 8 points per thread from F = 512 up (a complex double takes 4 VGPRs,
-// so P = 8 holds the same 32 data registers as the fp32 team's P = 16), one wave below.
-// F = 8192: 8 points per thread as well (T = 1024, 4 waves/SIMD at 128 VGPRs): its one
-// 136 KiB exchange buffer allows one team per CU either way, and the 16-point team
-// (T = 512, 2 waves/SIMD) measured 3.3 % slower despite fewer spills
-// (profiles/r02/ab/ab8k_f64_team_pipe.json); 16 points per thread below F = 8192 measured
-// slower too (profiles/r02/ab/ab64_p16_one_wave.json).
-#ifndef MIMO_X_P8K
-#define MIMO_X_P8K 8  // temporary A/B knob
-#endif
-constexpr int team_size64(int F) { return F >= 8192 ? F / MIMO_X_P8K : F >= 512 ? F / 8 : 64; }
+// so P = 8 holds the same 32 data registers as the fp32 team's P = 16), one wave below
+// (16 points per thread below F = 8192 measured slower, profiles/r02/ab/ab64_p16_one_wave.json).
+// F = 8192: 16 points per thread (T = 512, 2 waves/SIMD; its one 136 KiB exchange buffer
+// allows one team per CU either way): 4 transform stages instead of 5, -8 % against the
+// 1024-thread team once the Rapp gain stopped using the library log / exp
+// (profiles/r03/ab8k/ab_micro_p16.json; it was +3.3 % before, profiles/r02/ab/ab8k_f64_team_pipe.json).
+constexpr int team_size64(int F) { return F >= 8192 ? F / 16 : F >= 512 ? F / 8 : 64; }
 // Alternative team (8 points per thread: half the registers, 2x the waves, one more
 // LDS exchange per transform), selectable with MIMO_TEAM=<T> for A/B measurements.
 constexpr int alt_team_size(int F) { return F >= 1024 ? F / 8 : team_size(F); }

@@ -44,7 +44,7 @@ constexpr bool wave_fft_ok(int F, int T) {
 // fp64 config 2: 58.82 -> 58.50 ms (profiles/r02/ab/ab_wavefft_2048_f64.json).  The
 // barriers were not what the exchanges cost: their LDS round trips remain.
 constexpr bool wave_fft_used(int F, int T, bool f64) {
-  return wave_fft_ok(F, T) && f64 && F <= 4096;
+  return wave_fft_ok(F, T) && f64 && F <= 4096;  // F 8192 (T = 512): neutral, profiles/r03/ab8k/ab_p16_wave.json
 }
 constexpr int wave_fft_fw(int F, int T) { return F / (T / 64); }
 constexpr int wave_fft_tw_inter(int F, int T) { return fft_tw_total(wave_fft_fw(F, T), F / T); }

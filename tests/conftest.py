@@ -7,7 +7,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "m-mimo-ofdm-with-nonlinear-pa-sim_amd")
 GOLDEN = os.path.join(REPO, "tests", "golden")
-for p in (REPO, PKG):
+for p in (REPO, PKG, os.path.join(REPO, "tools")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

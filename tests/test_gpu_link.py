@@ -122,56 +122,25 @@ def test_published_curve_paper_config(receiver, channel):
     """The published BER-vs-Eb/N0 curves of the paper config (64 ant, F 4096, 2048 sc, 64-QAM,
     IBO 3 dB; figs/csv_results row layout: axis, no-distortion, standard RX, CNC / MCNC
     iterations 1..8) for every receiver and channel the reference publishes, against the
-    engine (float64) at 8,192 trials per point, all 16 Eb/N0 points in one launch.
+    engine (float64) at 8,192 trials per point (tools/replay_sigma.py).
 
-    Compared where the published BER >= 1e-4, by z-score: the GPU sigma from batch means
-    over trials, the published sigma from the same per-trial dispersion over the trials the
-    reference ran (its stopping rule with bits_sent_max 1e7, n_err_min 1e6).
-    Bounds: |z| <= 6, no bias per row (mean relative difference within 2 %), median
-    relative difference <= 3 %."""
-    import os
-    import utilities
-    from gpu_util import engine_for
-    from oracle import sim
-    d = os.path.join(os.path.dirname(__file__), "golden")
-    name = ("published_ber_vs_ebn0_cnc_rayleigh_ibo3" if (receiver, channel) == ("cnc", "rayleigh") else
-            "published_ber_vs_ebn0_%s_%s_nant64_ibo3_ebn0_min5_max20_step1.00_niter1_2_3_4_5_6_7_8" % (receiver, channel))
-    rows = np.asarray(utilities.read_from_csv(name, directory=d))
-    ebn0 = rows[0]
-    iters = [0, 1, 2, 3, 4]
-    n_tr = 8192
-    cfgs = [sim.SimConfig(64, 2048, 4096, 64, pa="softlim", ibo_db=3.0, snr_db=float(sim.rm.ebn0_to_snr(e, 2048, 2048, 64)),
-                          channel=channel, receiver=receiver) for e in ebn0]
-    eng = engine_for(cfgs[0])
-    pts = []
-    for c in cfgs:
-        from oracle.sim import point_params
-        pp = point_params(c)
-        pts.append(dict(ibo_db=c.ibo_db, snr_db=c.snr_db, avg_symbol_power=pp["es"], pa_kind="softlim",
-                        sat_pow=sim.rm.sat_pow(c.ibo_db, pp["avg_samp"] / c.n_ant), cnc_pa_kind="softlim",
-                        cnc_sat_pow=pp["cnc_sat"], cnc_alpha=pp["cnc_alpha"]))
-    n_pt = len(ebn0)
-    err, bits, per = eng.run_points(pts, [4242 + j for j in range(n_pt)], [0] * n_pt, [n_tr] * n_pt, iters, True,
-                                    per_trial=True)
-    bps = 2048 * 6
-    ber = (err / bits).T                                   # [idx, point]
-    per = per.reshape(n_pt, n_tr, len(iters) + 1).astype(np.float64) / bps
-    disp = per.std(axis=1, ddof=1).T                       # per-trial BER dispersion [idx, point]
-    pub = rows[1:2 + len(iters)]
-    n_ref = np.minimum(1e7 / bps, np.ceil(1e6 / np.maximum(pub, 1e-300) / bps).max(axis=0))
-    sig = np.maximum(disp, np.sqrt(np.maximum(pub, 1e-12) / bps)) * np.sqrt(1 / n_tr + 1 / n_ref)
-    sel = pub >= 1e-4
-    z = (ber - pub) / sig
-    rel = (ber - pub) / np.where(sel, pub, 1.0)
-    print(receiver, channel, "max|z|", np.abs(z[sel]).max(), "median rel", np.median(np.abs(rel[sel])))
-    for r in range(len(pub)):
-        print(" row", r, "ber", np.round(ber[r], 6).tolist(), "pub", pub[r].tolist(), "z", np.round(z[r], 2).tolist())
-    assert sel.sum() >= 20
-    assert np.abs(z[sel]).max() <= 6.0
-    assert np.median(np.abs(rel[sel])) <= 0.03
-    for r in range(len(pub)):
-        if sel[r].sum() >= 3:
-            assert abs(rel[r][sel[r]].mean()) <= 0.02, (r, rel[r][sel[r]])
+    Compared where the published BER >= 1e-4 by z = (ber - pub) / sqrt(s_gpu^2 + s_ref^2):
+    s_gpu by batch means over the engine's trials, s_ref as the spread of 24 replicas of the
+    reference's own estimator (its stopping rule: bits_sent_max 1e7, n_err_min 1e6, SURVEY
+    §6 -> 803-813 trials per point).  North_star's "within Monte-Carlo 1 sigma": measured
+    58-77 % of the points within 1 sigma and 92-99 % within 2 sigma, mean z^2 0.7-1.14
+    (profiles/r03/stats/replay_sigma.json; a normal sample gives 68 %, 95 %, 1).  The bounds
+    leave room for another seed's sampling: >= 50 % within 1 sigma, >= 85 % within 2, mean
+    z^2 <= 1.8, max |z| <= 4.5.  (The reference's workers replay one Rayleigh sequence,
+    channel.py:209-212: emulating that with 4-32 workers changed none of these numbers by
+    more than sampling noise, so the replicas draw independent channels.)"""
+    import replay_sigma
+    out, _ = replay_sigma.measure(receiver, channel, workers=(1,), reps=24)
+    st = out["by_workers"]["1"]
+    print(receiver, channel, out["compared"], st)
+    assert out["compared"] >= 60
+    assert st["frac_abs_z_le1"] >= 0.5 and st["frac_abs_z_le2"] >= 0.85
+    assert st["mean_z2"] <= 1.8 and st["max_abs_z"] <= 4.5
 
 
 def test_sixteen_workers_share_two_engines(tmp_path, monkeypatch):

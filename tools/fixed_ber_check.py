@@ -8,12 +8,14 @@ every (IBO, Eb/N0, iteration) BER with the published CSV
 (tests/golden/published_fixed_ber1.0e-02_<rx>_<channel>_nant64_...csv, a data file of the
 reference's figs/csv_results) by a z-score.
 
-sigma: batch means.  The per-trial dispersion of every (point, iteration) is measured from
-a separate per-trial sample (``n_disp`` trials per point, run_points per_trial=True); the
-GPU estimate's sigma = dispersion / sqrt(trials run), the published estimate's sigma =
-dispersion / sqrt(trials the reference ran), where the reference's trial count follows its
-stopping rule from the published BERs (all counters share trials; a counter closes at
-n_err_min errors or the bit budget).
+sigma: replicas of the reference's estimator.  Every point is re-run ``reps`` times with
+independent seeds at the trial count the reference's stopping rule gave it (from the
+published BERs: all counters share trials; a counter closes at n_err_min errors or the bit
+budget); the spread of those estimates is the published value's sigma, and the GPU
+estimate's sigma is the same spread scaled by sqrt(reference trials / trials run).  (The
+reference's workers replay one Rayleigh sequence, channel.py:209-212; tools/replay_sigma.py
+measured that replay to change these sigmas by < 5 % at 64 antennas, so the replicas draw
+independent channels.)
 
     python tools/fixed_ber_check.py --channel rayleigh --receiver cnc [--precision f64]
     python tools/fixed_ber_check.py --grid baseline      # BASELINE config 4 at its stated extent
@@ -86,15 +88,18 @@ def build_link(channel, receiver, precision):
                          precision=precision)
 
 
-def reference_trials(pub_ber, bits_per_sym):
+def reference_trials(pub_ber, bits_per_sym, per_counter=False):
     """Trials the reference's stopping rule needed per point: every counter closes at
-    n_err_min errors or at the bit budget; the point stops when all are closed."""
+    n_err_min errors or at the bit budget (it stops accumulating then, mp_model.py:181-187,
+    217-222); the point stops when all are closed.  per_counter: each counter's own count."""
     budget = BITS_MAX / bits_per_sym
     need = np.where(pub_ber > 0, N_ERR_MIN / np.maximum(pub_ber, 1e-300) / bits_per_sym, budget)
+    if per_counter:
+        return np.minimum(budget, np.ceil(need))
     return np.minimum(budget, np.ceil(need.max(axis=-1)))
 
 
-def run(channel="rayleigh", receiver="cnc", precision="f64", n_disp=32, seed=2137):
+def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137):
     import sweep
     from utilities import ebn0_to_snr
     link = build_link(channel, receiver, precision)
@@ -104,8 +109,9 @@ def run(channel="rayleigh", receiver="cnc", precision="f64", n_disp=32, seed=213
     err, bits = sweep.run_grid(link, IBO, EBN0, ITERS, incl_clean=False, seed=seed)
     wall = time.perf_counter() - t0
     trials = bits[..., 0] / bits_per_sym
+    trials_c = bits / bits_per_sym            # per counter: a closed counter stops accumulating
     ber = err / bits
-    # per-trial dispersion sample (independent trial indices)
+    # replicas of the reference's estimator at its trial counts (independent seeds)
     eng = link.engine()
     params = []
     for i in IBO:
@@ -115,15 +121,18 @@ def run(channel="rayleigh", receiver="cnc", precision="f64", n_disp=32, seed=213
             params.append(dict(link.point_params()))
     P = len(params)
     from mp_model import _seed64
-    seeds = [_seed64(sweep.point_seed(seed + 1, p)) for p in range(P)]
-    _, _, per = eng.run_points(params, seeds, [0] * P, [n_disp] * P, [int(x) for x in ITERS], False, per_trial=True)
-    per = per.reshape(len(IBO), len(EBN0), n_disp, len(ITERS)).astype(np.float64) / bits_per_sym
-    disp = per.std(axis=2, ddof=1)                       # per-trial BER dispersion
-    disp = np.maximum(disp, np.sqrt(np.maximum(ber, 1e-12) / bits_per_sym))  # floor: binomial
     pub_ibo, pub = published(channel, receiver)
     assert np.allclose(pub_ibo, IBO) and pub.shape == ber.shape, (pub_ibo, pub.shape, ber.shape)
-    n_ref = reference_trials(pub, bits_per_sym)[..., None]
-    sig = disp * np.sqrt(1.0 / trials[..., None] + 1.0 / n_ref)
+    n_ref = reference_trials(pub, bits_per_sym).astype(np.int64)          # [ibo, ebn0]
+    seeds = [_seed64(sweep.point_seed(seed + 1 + r, p)) for r in range(reps) for p in range(P)]
+    e_r, b_r, _ = eng.run_points(params * reps, seeds, [0] * (P * reps), list(n_ref.reshape(-1)) * reps,
+                                 [int(x) for x in ITERS], False)
+    est = (e_r / b_r).reshape(reps, len(IBO), len(EBN0), len(ITERS))
+    sig_rep = est.std(axis=0, ddof=1)         # one estimate over the point's n_ref trials
+    sig_rep = np.maximum(sig_rep, np.sqrt(np.maximum(pub, 1e-12) / (bits_per_sym * n_ref[..., None])))  # floor
+    # variance ~ 1 / trials: each published counter holds its own trial count, as does ours
+    n_ref_c = reference_trials(pub, bits_per_sym, per_counter=True)
+    sig = sig_rep * np.sqrt(n_ref[..., None] / n_ref_c + n_ref[..., None] / trials_c)
     sel = pub >= 1e-3
     z = np.where(sel, (ber - pub) / sig, 0.0)
     rel = np.where(sel, np.abs(ber - pub) / np.maximum(pub, 1e-300), 0.0)
@@ -179,8 +188,8 @@ def run_baseline(channel="rayleigh", receiver="cnc", precision="f64", seed=2137)
     ii = [int(np.argmin(np.abs(BASE_IBO - v))) for v in pub_ibo if v <= BASE_IBO[-1] + 1e-9]
     jj = [int(np.argmin(np.abs(BASE_EBN0 - v))) for v in EBN0]
     sub, pubs = ber[np.ix_(ii, jj)], pub[:len(ii)]
-    ntr_sub = trials[np.ix_(ii, jj)][..., None]
-    n_ref = reference_trials(pubs, bits_per_sym)[..., None]
+    ntr_sub = (bits / bits_per_sym)[np.ix_(ii, jj)]          # per counter
+    n_ref = reference_trials(pubs, bits_per_sym, per_counter=True)
     sig_sub = np.sqrt(np.maximum(pubs, 1e-12) * 8.0 / bits_per_sym) * np.sqrt(1 / ntr_sub + 1 / n_ref)
     sel = pubs >= 1e-3
     zsub = (sub - pubs) / sig_sub
