@@ -38,6 +38,11 @@ struct Profile {
 constexpr Profile profile_for(int T, bool aligned, int ch) {
   const int P = kF / T;
   if (kF64 && kF >= 8192) return Profile{2, 1, false};  // 136 KiB exchange buffer: one team per CU (T = 512: 2 waves/SIMD)
+  // fp64 up to F 2048: 3 waves/SIMD (168 VGPRs; the symbols rebuilt from the labels and
+  // |Hhat|^2 after the FFT, so 49.5 KiB of LDS per 256-thread team and 3 teams per CU):
+  // -8.5 % at config 2 (profiles/r03/ab_w3/).  F 4096 (8-wave teams, 84 KiB) cannot host a
+  // second team, so it stays at 2 waves/SIMD with the symbols in LDS.
+  if (kF64 && kF <= 2048) return Profile{3, 1, false};
   if (kF64) return Profile{2, 1, true};
   if (!aligned) return Profile{2, kF >= 4096 ? 1 : 2, true};  // one buffer from F = 4096: 2 teams/CU
   if (P < 16) return Profile{4, 2, false};

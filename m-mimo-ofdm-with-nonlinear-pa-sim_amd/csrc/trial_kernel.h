@@ -711,8 +711,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // in fp64); the opaque copies stop the compiler from hoisting it back out of the loop.
   // Register diet of the fp64 F = 8192 instance (-2.1 %; at F 2048 the |Hhat|^2 half measured
   // +0.8 %): symbols rebuilt from the labels per antenna, |Hhat|^2 recomputed after the FFT.
-  constexpr bool SYMW_RE = !SYMW_LDS && sizeof(R) == 8 && F >= 8192;  // off: +13 % at F 8192
-  constexpr bool E2_RE = sizeof(R) == 8 && F >= 8192;                  // off: +2.8 % (ab_diet_prefetch.json)
+  // (every fp64 instance without symbols in LDS: F <= 2048 at 3 waves/SIMD, F 8192)
+  constexpr bool SYMW_RE = !SYMW_LDS && sizeof(R) == 8;  // off: +13 % at F 8192
+  constexpr bool E2_RE = sizeof(R) == 8 && !SYMW_LDS;    // off: +2.8 % at F 8192 (ab_diet_prefetch.json)
   C symw_r[SYMW_LDS || SYMW_RE ? 1 : NSLOT];
   uint32_t slab_r[SYMW_RE ? NSLOT : 1];
   auto set_symbols = [&](const uint32_t (&lab_in)[NSLOT]) __attribute__((always_inline)) {
