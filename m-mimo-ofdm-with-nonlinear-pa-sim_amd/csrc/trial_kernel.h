@@ -344,6 +344,17 @@ __device__ __forceinline__ cx<R> qam_point(uint32_t label, int L, int hb) {
   const uint32_t ii = gray_inv(label >> hb), iq = gray_inv(label & ((1u << hb) - 1u));
   return mkc((R)(2 * (int)ii - (L - 1)), (R)(2 * (int)iq - (L - 1)));
 }
+// The same point as two int16 lattice levels in one word (I high, Q low): the register
+// diet keeps these per slot and rebuilds the point per antenna in 2 shifts + 2 converts
+// instead of the two inverse Gray codes (~20 integer ops).
+__device__ __forceinline__ uint32_t qam_levels(uint32_t label, int L, int hb) {
+  const int ii = 2 * (int)gray_inv(label >> hb) - (L - 1), iq = 2 * (int)gray_inv(label & ((1u << hb) - 1u)) - (L - 1);
+  return ((uint32_t)ii << 16) | ((uint32_t)iq & 0xFFFFu);
+}
+template <typename R>
+__device__ __forceinline__ cx<R> levels_point(uint32_t v) {
+  return mkc((R)((int)v >> 16), (R)(int)(int16_t)(v & 0xFFFFu));
+}
 
 // ---------------------------------------------------------------- channel generation
 // sin / cos of a channel phase in revolutions: fp32 hardware (v_sin / v_cos take
@@ -706,8 +717,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // MAIN: symbols = tx labels, combine with the true channel, accumulate g (alpha_a).
   // MCNC: symbols = detected labels, combine with the estimated channel (corrector.py:198-200).
   // The symbols enter pre-weighted, symw = s / ||Hhat|| / sqrt(F) (0 on invalid slots).
-  // SYMW_RE (register diet, symbols not in LDS): keep the labels
-  // (1 VGPR per slot) and rebuild the symbol per antenna instead of holding it (4 VGPRs
+  // SYMW_RE (register diet, symbols not in LDS): keep the lattice levels (qam_levels,
+  // 1 VGPR per slot) and rebuild the symbol per antenna instead of holding it (4 VGPRs
   // in fp64); the opaque copies stop the compiler from hoisting it back out of the loop.
   // Register diet of the fp64 F = 8192 instance (-2.1 %; at F 2048 the |Hhat|^2 half measured
   // +0.8 %): symbols rebuilt from the labels per antenna, |Hhat|^2 recomputed after the FFT.
@@ -720,7 +731,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
       if constexpr (SYMW_RE) {
-        slab_r[s] = lab_in[s];
+        slab_r[s] = qam_levels(lab_in[s], L, hb);
       } else {
         const C v = cscale(qam_point<R>(lab_in[s], L, hb), inv_nrm[s] * inv_sqrt_f);
         if constexpr (SYMW_LDS) symw_s[s * T + t] = v; else symw_r[s] = v;
@@ -732,7 +743,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       uint32_t l = slab_r[s];
       R in = inv_nrm[s];
       asm volatile("" : "+v"(l), "+v"(in));
-      return cscale(qam_point<R>(l, L, hb), in * inv_sqrt_f);
+      return cscale(levels_point<R>(l), in * inv_sqrt_f);
     } else if constexpr (SYMW_LDS) {
       return symw_s[s * T + t];
     } else {
