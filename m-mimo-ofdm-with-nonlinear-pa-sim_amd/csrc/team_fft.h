@@ -231,7 +231,8 @@ struct TeamFft {
   // of the 1/16 layout exactly, profiles/r02/pmc_f64_r1).  F = 8192 keeps 1/16: its 16 KiB
   // more would not fit the 160 KiB LDS next to the fp64 tables and the CSI scratch.
   static constexpr int PADN = 5;  // one pad slot per 32 elements for exchanges >= 1
-  static constexpr int PAD0 = (sizeof(Re) == 8 && F < 8192) ? 3 : 4;
+  // (fp64 F 4096 on 256 threads: 1/32, so that two teams fit a CU -- 80,256 B each)
+  static constexpr int PAD0 = (sizeof(Re) == 8 && F < 8192) ? (F == 4096 && T == 256 ? 5 : 3) : 4;
   static constexpr int psh(int S) { return S == 0 ? PAD0 : PADN; }
   static constexpr int LDS_ELEMS = F + F / (1 << (PAD0 < PADN ? PAD0 : PADN));
   static_assert((1 << LOG_F) == F && (1 << LOG_P) == P && P >= 2, "power-of-two sizes");

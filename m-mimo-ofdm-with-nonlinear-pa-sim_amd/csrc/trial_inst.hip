@@ -43,6 +43,7 @@ constexpr Profile profile_for(int T, bool aligned, int ch) {
   // -8.5 % at config 2 (profiles/r03/ab_w3/).  F 4096 (8-wave teams, 84 KiB) cannot host a
   // second team, so it stays at 2 waves/SIMD with the symbols in LDS.
   if (kF64 && kF <= 2048) return Profile{3, 1, false};
+  if (kF64 && kF == 4096) return Profile{2, 1, false};  // 16-point team, symbols from levels: 2 teams/CU
   if (kF64) return Profile{2, 1, true};
   if (!aligned) return Profile{2, kF >= 4096 ? 1 : 2, true};  // one buffer from F = 4096: 2 teams/CU
   if (P < 16) return Profile{4, 2, false};

@@ -15,7 +15,10 @@ constexpr int team_size(int F) { return F >= 1024 ? F / 16 : 64; }
 // allows one team per CU either way): 4 transform stages instead of 5, -8 % against the
 // 1024-thread team once the Rapp gain stopped using the library log / exp
 // (profiles/r03/ab8k/ab_micro_p16.json; it was +3.3 % before, profiles/r02/ab/ab8k_f64_team_pipe.json).
-constexpr int team_size64(int F) { return F >= 8192 ? F / 16 : F >= 512 ? F / 8 : 64; }
+// F = 4096: 16 points per thread as well (T = 256, 3 stages, two 4-wave teams per CU at
+// 80 KiB of LDS each): -29 % against the 512-thread wave-split team on the paper config
+// (69.80 -> 49.66 ms per 32,768 trials, profiles/r03/ab_4k/).
+constexpr int team_size64(int F) { return F >= 4096 ? F / 16 : F >= 512 ? F / 8 : 64; }
 // Alternative team (8 points per thread: half the registers, 2x the waves, one more
 // LDS exchange per transform), selectable with MIMO_TEAM=<T> for A/B measurements.
 constexpr int alt_team_size(int F) { return F >= 1024 ? F / 8 : team_size(F); }

@@ -31,20 +31,21 @@
 
 namespace mimo {
 
-
 // The plan needs at least two waves and whole radix-WV butterflies per thread.
 constexpr bool wave_fft_ok(int F, int T) {
   return T >= 128 && T % 64 == 0 && (F / T) >= (T / 64) && (F / T) % (T / 64) == 0;
 }
-// Instances that use it (kernel and engine): fp64 up to F = 4096 (F = 8192's padded rows
-// would not fit the 160 KiB LDS next to the fp64 tables).  fp32: not used (F = 8192's 8-wave
+// Instances that use it (kernel and engine): fp64 up to F = 2048.  fp32: not used (F = 8192's 8-wave
 // teams measured 17.43 -> 17.64 ms with it, profiles/r02/ab/ab_wavefft_8192_f32.json; below
 // F = 8192 the 2-wave fp32 teams need only two exchanges per transform, which the split
 // would raise to three).
 // fp64 config 2: 58.82 -> 58.50 ms (profiles/r02/ab/ab_wavefft_2048_f64.json).  The
 // barriers were not what the exchanges cost: their LDS round trips remain.
 constexpr bool wave_fft_used(int F, int T, bool f64) {
-  return wave_fft_ok(F, T) && f64 && F <= 4096;  // F 8192 (T = 512): neutral, profiles/r03/ab8k/ab_p16_wave.json
+  // F 4096 / 8192 run 16-point teams (trial_launch.h team_size64) on the team FFT: the
+  // wave-split rows would not leave room for a second team at F 4096, and measured
+  // neutral at F 8192 (profiles/r03/ab8k/ab_p16_wave.json).
+  return wave_fft_ok(F, T) && f64 && F <= 2048;
 }
 constexpr int wave_fft_fw(int F, int T) { return F / (T / 64); }
 constexpr int wave_fft_tw_inter(int F, int T) { return fft_tw_total(wave_fft_fw(F, T), F / T); }
