@@ -12,13 +12,14 @@ Compared at every (point, iteration) with published BER >= 1e-3 (tools/fixed_ber
   its stopping-rule trial counts (per counter: a counter closes at n_err_min errors or the
   bit budget), the GPU estimate's from the same spread at its own trial counts.  Measured
   (profiles/r03/stats/config4_sigma.log): 47-58 % within 1 sigma, 82-85 % within 2,
-  p95 |z| 2.9-3.1, mean z^2 2.0-2.5 -- about 1.4x the spread the replicas predict.  Not
-  explained yet: the reference's channel replay (channel.py:209-212) measured no effect at
-  64 antennas (profiles/r03/stats/replay_sigma.json), and the published BER-vs-Eb/N0
-  curves (fixed 813-trial budgets) show plain 1-sigma statistics (tests/test_gpu_link.py);
-  candidates are the grids' data-dependent stop at 1e5 errors on ~150-400 trials and the
-  heavy tail of per-trial BER, which 16 replicas under-read.  Bounds: >= 75 % within 2 sigma, p95 |z| <= 3.5,
-  mean z^2 <= 3, max |z| <= 8;
+  p95 |z| 2.9-3.1, mean z^2 2.0-2.5 -- about 1.4x the spread the replicas predict.  The
+  replica sigma is right for this estimator (one replica against the other 15: 67 % within
+  1 sigma, 94 % within 2; profiles/r03/stats/config4_self_check.log), so the excess is in
+  the published estimates; the reference's channel replay (channel.py:209-212) measured no
+  effect at 64 antennas (profiles/r03/stats/replay_sigma.json), and the published
+  BER-vs-Eb/N0 curves show plain 1-sigma statistics (tests/test_gpu_link.py).  Bounds:
+  >= 75 % within 2 sigma, p95 |z| <= 3.5, mean z^2 <= 3, max |z| <= 8; the replica
+  self-check >= 90 % within 2 sigma;
 * the derived curve itself (Eb/N0 needed for BER 1e-2 per IBO and iteration): reachable
   exactly where the published grid reaches it, mean |difference| <= 0.1 dB (measured
   0.01-0.05 dB).
@@ -45,6 +46,7 @@ def test_fixed_ber_grid_vs_published(receiver, channel):
     assert out["median_rel"] <= 0.02
     assert out["frac_abs_z_le2"] >= 0.75 and out["p95_abs_z"] <= 3.5
     assert out["mean_z2"] <= 3.0 and out["max_abs_z"] <= 8.0
+    assert out["replica_self_check"]["frac_abs_z_le2"] >= 0.9
     r = out["req_ebn0_at_ber_1e2"]
     assert r["finite_mismatch"] == 0 and r["compared"] >= 70 and r["mean_abs_db"] <= 0.1
 

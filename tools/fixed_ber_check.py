@@ -133,6 +133,10 @@ def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137)
     # variance ~ 1 / trials: each published counter holds its own trial count, as does ours
     n_ref_c = reference_trials(pub, bits_per_sym, per_counter=True)
     sig = sig_rep * np.sqrt(n_ref[..., None] / n_ref_c + n_ref[..., None] / trials_c)
+    # self-consistency of the replica sigma: the last replica against the mean of the others
+    # (same trial counts, same sigma model) -- a normal sample puts ~95 % within 2 sigma
+    s_loo = est[:-1].std(axis=0, ddof=1)
+    z_self = (est[-1] - est[:-1].mean(axis=0)) / np.maximum(s_loo * np.sqrt(1.0 + 1.0 / (reps - 1)), 1e-300)
     sel = pub >= 1e-3
     z = np.where(sel, (ber - pub) / sig, 0.0)
     rel = np.where(sel, np.abs(ber - pub) / np.maximum(pub, 1e-300), 0.0)
@@ -151,6 +155,8 @@ def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137)
                frac_abs_z_gt3=round(float((np.abs(z[sel]) > 3).mean()), 5),
                frac_abs_z_le1=round(float((np.abs(z[sel]) <= 1).mean()), 4),
                frac_abs_z_le2=round(float((np.abs(z[sel]) <= 2).mean()), 4),
+               replica_self_check=dict(frac_abs_z_le1=round(float((np.abs(z_self[sel]) <= 1).mean()), 4),
+                                       frac_abs_z_le2=round(float((np.abs(z_self[sel]) <= 2).mean()), 4)),
                median_rel=round(float(np.median(rel[sel])), 5), max_rel=round(float(rel[sel].max()), 4),
                worst=dict(ibo=float(IBO[worst[0]]), ebn0=float(EBN0[worst[1]]), iteration=int(worst[2]),
                           ber=float(ber[worst]), published=float(pub[worst]), z=float(z[worst])),
