@@ -36,20 +36,58 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t k) {
 // instruction) + 2 x v_bitop3_b32, instead of mul_hi + mul_lo + 2 xor per word: every
 // 32-bit integer op is half rate on gfx950 (tools/microbench/ops.hip).  The key words are
 // uniform (SGPRs), the one scalar operand a VOP3 op may take.
+
+// UNI = true: every call site's counter words 1-3 (trial, stream, antenna) are
+// wave-uniform, so rounds 0-2 are written in plain C where a uniform operand meets the
+// round: the compiler keeps those products and xors on the SALU (round 0: M1 c.z; round 1:
+// M0 c.x) and needs one v_xor where bitop3 would first copy the uniform word into a VGPR;
+// rounds 3-9 are per-lane throughout.  Measured: -1.2 % at F 2048 and -4 % on the CSI
+// instance, but +1.7 % / +1.4 % at F 4096 / 8192 (profiles/r03/ab_o, ab_p), so the
+// trial kernel takes it for the fp64 wave-split instances only (Channel::kUni).
+template <bool UNI = false>
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, Key key) {
-  uint32_t k0 = key.k0, k1 = key.k1;
+  if constexpr (!UNI) {
+    uint32_t k0 = key.k0, k1 = key.k1;
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    if (r) {
-      k0 += 0x9E3779B9u;
-      k1 += 0xBB67AE85u;
+    for (int r = 0; r < 10; ++r) {
+      if (r) {
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+      }
+      const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+      const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+      c = make_uint4(xor3((uint32_t)(p1 >> 32), c.y, k0), (uint32_t)p1, xor3((uint32_t)(p0 >> 32), c.w, k1),
+                     (uint32_t)p0);
     }
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
-    c = make_uint4(xor3((uint32_t)(p1 >> 32), c.y, k0), (uint32_t)p1, xor3((uint32_t)(p0 >> 32), c.w, k1),
+    return c;
+  } else {
+    constexpr uint32_t kW0 = 0x9E3779B9u, kW1 = 0xBB67AE85u;
+    const uint32_t k0 = key.k0, k1 = key.k1;
+    // round 0: c.y, c.z, c.w uniform (readfirstlane keeps c.w ^ k1 one SGPR operand; the
+    // compiler would otherwise re-associate it into two v_xor)
+    uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t wk = (uint32_t)__builtin_amdgcn_readfirstlane((int)(c.w ^ k1));
+    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ wk, (uint32_t)p0);
+    // round 1: c.x, c.y uniform
+    p0 = (uint64_t)0xD2511F53u * c.x;
+    p1 = (uint64_t)0xCD9E8D57u * c.z;
+    c = make_uint4((uint32_t)(p1 >> 32) ^ (c.y ^ (k0 + kW0)), (uint32_t)p1, ((uint32_t)(p0 >> 32) ^ (k1 + kW1)) ^ c.w,
                    (uint32_t)p0);
+    // round 2: c.w uniform
+    p0 = (uint64_t)0xD2511F53u * c.x;
+    p1 = (uint64_t)0xCD9E8D57u * c.z;
+    c = make_uint4(xor3((uint32_t)(p1 >> 32), c.y, k0 + 2u * kW0), (uint32_t)p1,
+                   (uint32_t)(p0 >> 32) ^ (c.w ^ (k1 + 2u * kW1)), (uint32_t)p0);
+#pragma unroll
+    for (int r = 3; r < 10; ++r) {
+      p0 = (uint64_t)0xD2511F53u * c.x;
+      p1 = (uint64_t)0xCD9E8D57u * c.z;
+      c = make_uint4(xor3((uint32_t)(p1 >> 32), c.y, k0 + (uint32_t)r * kW0), (uint32_t)p1,
+                     xor3((uint32_t)(p0 >> 32), c.w, k1 + (uint32_t)r * kW1), (uint32_t)p0);
+    }
+    return c;
   }
-  return c;
 }
 
 // Box-Muller on two words -> CN(0,1):  sqrt(-ln u1) * exp(j 2 pi u2),
@@ -97,20 +135,20 @@ __device__ __forceinline__ double2 box_muller(uint32_t w0, uint32_t w1, double c
   return make_double2(rho * co, rho * s);
 }
 
-template <class C>
+template <bool UNI = false, class C>
 __device__ __forceinline__ void cn_pair(Key key, uint32_t q, uint32_t trial, uint32_t stream, uint32_t aux, C& z1,
                                         C& z2, real_of<C> c) {
-  const uint4 w = philox4x32_10(make_uint4(q, trial, stream, aux), key);
+  const uint4 w = philox4x32_10<UNI>(make_uint4(q, trial, stream, aux), key);
   z1 = box_muller(w.x, w.y, c);
   z2 = box_muller(w.z, w.w, c);
 }
 
 // |z1|^2, |z2|^2 of cn_pair's draws without forming them: rho^2 = c log(u1) (one log
 // per draw; no sqrt / sin / cos).  MRT norms only need the channel power.
-template <typename R>
+template <bool UNI = false, typename R>
 __device__ __forceinline__ void cn_pair_pow(Key key, uint32_t q, uint32_t trial, uint32_t stream, uint32_t aux, R& p1,
                                             R& p2, R c) {
-  const uint4 w = philox4x32_10(make_uint4(q, trial, stream, aux), key);
+  const uint4 w = philox4x32_10<UNI>(make_uint4(q, trial, stream, aux), key);
   p1 = c * bm_log(w.x, R(0));
   p2 = c * bm_log(w.z, R(0));
 }
@@ -124,8 +162,9 @@ __device__ __forceinline__ void pair_of(int k, int n_sc, uint32_t& q, int& slot)
   q = (uint32_t)(h * quarter + r - slot * quarter);
 }
 
+template <bool UNI = false>
 __device__ __forceinline__ uint32_t qam_label(Key key, int k, uint32_t trial, uint32_t mask) {
-  const uint4 w = philox4x32_10(make_uint4((uint32_t)k >> 2, trial, ST_BITS, 0u), key);
+  const uint4 w = philox4x32_10<UNI>(make_uint4((uint32_t)k >> 2, trial, ST_BITS, 0u), key);
   const int s = k & 3;
   const uint32_t word = s == 0 ? w.x : s == 1 ? w.y : s == 2 ? w.z : w.w;
   return word & mask;

@@ -92,16 +92,21 @@ static __shared__ double2 lut64[kLut64];
 // sin / cos of 2 pi w 2^-32 (w: a uint32 word, revolutions): i = nearest 256th,
 // phi = 2 pi (w - i 2^24) 2^-32 in [-pi/256, pi/256], series to phi^7 / phi^6 and the
 // angle sum with the table's (cos, sin)(2 pi i / 256).  <= ~1.5 ulp.
+// The series run in the integer residual f itself (coefficients scaled by powers of
+// h = 2 pi 2^-32): sin = f (h - h^3 f^2 / 6 + ...), cos = 1 - h^2 f^2 / 2 + ... -- one
+// multiply fewer than forming phi = h f first.
 __device__ __forceinline__ void sincos_lut(uint32_t w, double& sn, double& cs) {
   const uint32_t i = (w + 0x800000u) >> 24;  // wraps to 0 near a full revolution
-  const int f = (int)(w - (i << 24));        // [-2^23, 2^23)
-  const double phi = (double)f * 1.4629180792671596e-09;  // 2 pi 2^-32
-  const double z = phi * phi;
-  double ps = fma(z, -1.0 / 5040, 1.0 / 120);
-  ps = fma(ps, z, -1.0 / 6);
-  const double s = fma(phi * z, ps, phi);
-  double pc = fma(z, -1.0 / 720, 1.0 / 24);
-  pc = fma(pc, z, -0.5);
+  const double f = (double)(int)(w - (i << 24));  // [-2^23, 2^23), exact
+  constexpr double h = 1.4629180792671596e-09;    // 2 pi 2^-32
+  constexpr double h2 = h * h;
+  const double z = f * f;                         // exact (< 2^46)
+  double ps = fma(z, -(h2 * h2 * h2 * h) / 5040, (h2 * h2 * h) / 120);
+  ps = fma(ps, z, -(h2 * h) / 6);
+  ps = fma(ps, z, h);
+  const double s = f * ps;
+  double pc = fma(z, -(h2 * h2 * h2) / 720, (h2 * h2) / 24);
+  pc = fma(pc, z, -h2 / 2);
   const double c = fma(z, pc, 1.0);
   const double2 cst = lut64[kLnTab + (i & 255u)];
   sn = fma(cst.y, c, cst.x * s);

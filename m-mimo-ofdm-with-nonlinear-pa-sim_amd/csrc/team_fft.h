@@ -165,6 +165,30 @@ struct Dft {
       v[2] = zsub<z02, z13>(t0, t2);
       v[1] = zadd<z02, z13>(t1, t3);
       v[3] = zsub<z02, z13>(t1, t3);
+    } else if constexpr (R == 8) {
+      // 2 x 4: two DFT-4s, then the DFT-2s with W8^k2 on the odd half.  The odd-multiple-
+      // of-pi/4 rotations W8^1, W8^3 are c (+-x.x +- x.y, +-x.x +- x.y), c = 1/sqrt(2):
+      // two adds, and c goes into the DFT-2 as an FMA (6 ops instead of 4 + 4).
+      C sub[2][4];
+      first_level<0, 2, 4>(sub, v);
+      using Re = real_of<C>;
+      constexpr Re c = (Re)0.70710678118654752440084436210484903928;
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) {
+        const C a = sub[0][k2], x = sub[1][k2];
+        if (k2 == 0 || k2 == 2) {
+          const C b = k2 == 0 ? x : ctw<2, 8, DIR>(x);
+          v[k2] = cadd(a, b);
+          v[k2 + 4] = csub(a, b);
+        } else {
+          // x e^{DIR j 2pi k2 / 8} = c u
+          C u;
+          if (k2 == 1) u = DIR < 0 ? mkc(x.x + x.y, x.y - x.x) : mkc(x.x - x.y, x.x + x.y);
+          else u = DIR < 0 ? mkc(x.y - x.x, -x.x - x.y) : mkc(-x.x - x.y, x.x - x.y);
+          v[k2] = mkc(fmar(c, u.x, a.x), fmar(c, u.y, a.y));
+          v[k2 + 4] = mkc(fmar(-c, u.x, a.x), fmar(-c, u.y, a.y));
+        }
+      }
     } else {
       constexpr int R1 = (R >= 16) ? 4 : 2;
       constexpr int R2 = R / R1;
@@ -215,7 +239,10 @@ __device__ __forceinline__ void xchg_sync() {
 }
 
 // ---------------------------------------------------------------- team FFT
-template <int F, int T, int NBUF = 2, typename Re = float, bool WAVE = false>
+// LTW1: stage 1's twiddle block comes from an LDS copy (run()'s tw1 argument; the wave-split
+// FFT's one-wave sub-transforms, whose stage-1 block is small: 64 entries at F 2048) -- all
+// R - 1 twiddles read, none formed as products (fp64: 16 VALU ops per stage saved).
+template <int F, int T, int NBUF = 2, typename Re = float, bool WAVE = false, bool LTW1 = false>
 struct TeamFft {
   using C = cx<Re>;
   static constexpr int P = F / T;
@@ -240,6 +267,8 @@ struct TeamFft {
 
   static constexpr int bits(int s) { return fft_bits(F, P, s); }
   static constexpr int bits_before(int s) { return fft_bits_before(F, P, s); }
+  // entries of stage 1's [R][NS] twiddle block (offset 0 of the table)
+  static constexpr int TW1_N = NST > 1 ? (1 << fft_bits(F, P, 1)) * (1 << fft_bits_before(F, P, 1)) : 1;
   template <int S>
   static __host__ __device__ constexpr int pad(int e) { return e + (e >> psh(S)); }
   // Global-address-space load (the laundered table pointer would otherwise be generic
@@ -353,7 +382,7 @@ struct TeamFft {
     if constexpr (S < NST) {
       constexpr int R = 1 << bits(S);
       constexpr int NS = 1 << bits_before(S);
-      if constexpr (NS > 1) {
+      if constexpr (NS > 1 && !(LTW1 && S == 1)) {
         constexpr int TW_OFF = fft_tw_off(F, P, S);
         const int jm0 = t & (NS - 1);
 #pragma unroll
@@ -367,7 +396,8 @@ struct TeamFft {
 
   template <int S, int DIR, int PAR, uint32_t ZM, typename Fill>
   static __device__ __forceinline__ void stage(C (&d)[P], C* lds, const C* __restrict__ tw, int t,
-                                               bool no_xchg, const Base& base, const Fill& fill) {
+                                               bool no_xchg, const Base& base, const Fill& fill,
+                                               const C* tw1) {
     constexpr int R = 1 << bits(S);
     constexpr int NS = 1 << bits_before(S);
     constexpr int B = P / R;
@@ -375,7 +405,11 @@ struct TeamFft {
     static_assert(B >= 1 && B * R == P, "radix must divide points per thread");
     C* buf = lds + (NBUF == 2 ? ((S + PAR) & 1) * LDS_ELEMS : 0);
     C w0[R];
-    if constexpr (NS > 1 && PREFETCH) {
+    if constexpr (NS > 1 && LTW1 && S == 1) {
+      const C* tws = tw1 + (t & (NS - 1));
+#pragma unroll
+      for (int r = 1; r < R; ++r) w0[r] = tws[r * NS];
+    } else if constexpr (NS > 1 && PREFETCH) {
 #pragma unroll
       for (int r = 1; r < R; ++r) {
         if ((r & (r - 1)) == 0) {
@@ -417,10 +451,10 @@ struct TeamFft {
 
   template <int S, int DIR, int PAR, uint32_t ZM, typename Fill>
   static __device__ __forceinline__ void stages(C (&d)[P], C* lds, const C* __restrict__ tw, int t,
-                                                bool no_xchg, const Base& base, const Fill& fill) {
+                                                bool no_xchg, const Base& base, const Fill& fill, const C* tw1) {
     if constexpr (S < NST) {
-      stage<S, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base, fill);
-      stages<S + 1, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base, fill);
+      stage<S, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base, fill, tw1);
+      stages<S + 1, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base, fill, tw1);
     }
   }
 
@@ -443,20 +477,22 @@ struct TeamFft {
   };
   template <int DIR, int PAR = 0, uint32_t ZM = 0, typename Fill = NoFill>
   static __device__ __forceinline__ void run(C (&d)[P], C* lds, const C* __restrict__ tw, int t,
-                                             bool no_xchg = false, const Fill& fill = Fill{}) {
+                                             bool no_xchg = false, const Fill& fill = Fill{},
+                                             const C* tw1 = nullptr) {
     const C* twl = tw;
     int tl = t;
     asm volatile("" : "+s"(twl));
     asm volatile("" : "+v"(tl));
     Base base;
     if constexpr (PREFETCH) load_base<1>(base, twl, tl);
-    stages<0, DIR, PAR, ZM>(d, lds, twl, tl, no_xchg, base, fill);
+    stages<0, DIR, PAR, ZM>(d, lds, twl, tl, no_xchg, base, fill, tw1);
   }
   // IFFT then FFT of one antenna / CNC iteration: an even number of exchanges in total.
   template <int DIR, typename Fill = NoFill>
   static __device__ __forceinline__ void run_second(C (&d)[P], C* lds, const C* __restrict__ tw, int t,
-                                                    bool no_xchg = false, const Fill& fill = Fill{}) {
-    run<DIR, XCHG & 1, 0u, Fill>(d, lds, tw, t, no_xchg, fill);
+                                                    bool no_xchg = false, const Fill& fill = Fill{},
+                                                    const C* tw1 = nullptr) {
+    run<DIR, XCHG & 1, 0u, Fill>(d, lds, tw, t, no_xchg, fill, tw1);
   }
 };
 

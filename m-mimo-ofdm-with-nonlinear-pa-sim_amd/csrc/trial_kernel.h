@@ -40,7 +40,6 @@ enum PaKind : int { PA_NONE = 0, PA_SOFTLIM = 1, PA_RAPP = 2, PA_TOI = 3 };
 enum ChanKind : int { CH_RAYLEIGH = 1, CH_LOS = 2, CH_TWOPATH = 3, CH_TABLE = 4 };
 enum RxKind : int { RX_CNC = 1, RX_MCNC = 2 };
 
-constexpr int kMaxWaves = 16;
 constexpr int kMaxCsiAnt = 512;  // CSI-error runs: antennas (LDS per team; engine.hip checks)
 constexpr uint32_t kFixedCsiTrial = 0xFFFFFFFFu;  // CSI stream counter of fixed-channel runs (oracle/sim.py draws)
 // The measured alternatives of the choices below (channel pipeline on / off per precision,
@@ -72,10 +71,12 @@ struct TrialParams {
   // fp32 instances only: the fp64 instances always evaluate the exact formula.
   R apoly[9];
   R inv_vk0, alpha_xlim;
-  // fp64 instances: alpha(gamma_a^2) as a Chebyshev series of degree 18 in t = x / alpha_xlim
-  // (Clenshaw; the host fits it at 64 nodes in double: ~1e-16 relative, the singularity of
-  // alpha(g0^2 / (1 + x)) at x = -1 is 4 half-widths away), the exact formula outside.
-  double acheb[19];
+  R inv_vk0_f;                   // inv_vk0 F (the fp64 register-diet array pass sums vk / F)
+  // fp64 instances: alpha(gamma_a^2) as a degree-18 polynomial in x on |x| <= alpha_xlim
+  // (the host's Chebyshev interpolant at 64 nodes in long double, as monomials: Horner,
+  // <= 1.6e-16 relative; the singularity of alpha(g0^2 / (1 + x)) at x = -1 is 4
+  // half-widths away), the exact formula outside.
+  double amono64[19];
   R es_over_snr;                 // Es / 10^(SNR/10)
   R csi_a, csi_b;                // sqrt(1 - eps^2), eps
   R inv_sqrt_f;
@@ -186,16 +187,19 @@ __device__ __forceinline__ R wave_sum(R v) {
 // VALU instead of the six dependent ds_bpermute round trips of __shfl_xor.  Per row of
 // 16 lanes: pair / quad swaps and the half-row / row mirrors give every lane its row sum;
 // row_bcast:15 then row_bcast:31 fold rows 0-2 into row 3.  (fp64: both halves moved.)
+// mov_dpp leaves the lanes of disabled rows undefined (no zero-initialised "old" operand,
+// one v_mov fewer per step): after the row_bcast:15 step rows 0 and 2 hold garbage, which
+// no later step reads (row_bcast:31 reads lane 31, row 1) and lane 63 never sees.
 template <int CTRL, int ROW_MASK = 0xF>
 __device__ __forceinline__ float dpp_add(float v) {
-  const int s = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, false);
+  const int s = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, false);
   return v + __builtin_bit_cast(float, s);
 }
 template <int CTRL, int ROW_MASK = 0xF>
 __device__ __forceinline__ double dpp_add(double v) {
   const uint64_t u = __builtin_bit_cast(uint64_t, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, ROW_MASK, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, ROW_MASK, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, ROW_MASK, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, ROW_MASK, 0xF, false);
   return v + __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 template <typename R>
@@ -369,6 +373,8 @@ __device__ __forceinline__ void sincos_phase(double r, double& sn, double& cs) {
 
 template <typename R, int F, int T, int NSLOT, bool ALIGNED, int CH>
 struct Channel {
+  // philox.h UNI rounds: the fp64 wave-split instances (F <= 2048) only
+  static constexpr bool kUni = sizeof(R) == 8 && wave_fft_used(F, T, true);
   using SL = Slots<F, T, NSLOT, ALIGNED>;
   using C = cx<R>;
   using Params = TrialParams<R>;
@@ -389,10 +395,10 @@ struct Channel {
       for (int j = 0; j < Q; ++j) {
         C z1, z2;
         const bool sw = (j == 0) && t0;
-        cn_pair(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, stream, aux, z1, z2, c);
+        cn_pair<kUni>(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, stream, aux, z1, z2, c);
         z[j] = sw ? z2 : z1;
         z[j + Q] = sw ? z1 : z2;
-        cn_pair(key, (uint32_t)(t + T * j), trial, stream, aux, z1, z2, c);
+        cn_pair<kUni>(key, (uint32_t)(t + T * j), trial, stream, aux, z1, z2, c);
         z[SL::HALF + j] = z1;
         z[SL::HALF + j + Q] = z2;
       }
@@ -407,7 +413,7 @@ struct Channel {
           int slot;
           pair_of(k, S, q, slot);
           C z1, z2;
-          cn_pair(key, q, trial, stream, aux, z1, z2, c);
+          cn_pair<kUni>(key, q, trial, stream, aux, z1, z2, c);
           z[s] = slot == 0 ? z1 : z2;
         }
       }
@@ -426,12 +432,12 @@ struct Channel {
       C z1, z2;
       if ((c & 1) == 0) {
         const bool sw = (j == 0) && (t == 0);
-        cn_pair(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)((S >> 2) - 1 + t + T * j), trial, stream, aux, z1, z2,
+        cn_pair<kUni>(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)((S >> 2) - 1 + t + T * j), trial, stream, aux, z1, z2,
                 cs);
         z[j] = sw ? z2 : z1;
         z[j + Q] = sw ? z1 : z2;
       } else {
-        cn_pair(key, (uint32_t)(t + T * j), trial, stream, aux, z1, z2, cs);
+        cn_pair<kUni>(key, (uint32_t)(t + T * j), trial, stream, aux, z1, z2, cs);
         z[SL::HALF + j] = z1;
         z[SL::HALF + j + Q] = z2;
       }
@@ -454,11 +460,11 @@ struct Channel {
       for (int j = 0; j < Q; ++j) {
         R p1, p2;
         const bool sw = (j == 0) && t0;
-        cn_pair_pow(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, ST_CHAN, (uint32_t)a, p1, p2,
+        cn_pair_pow<kUni>(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, ST_CHAN, (uint32_t)a, p1, p2,
                     c);
         e2[j] = sw ? p2 : p1;
         e2[j + Q] = sw ? p1 : p2;
-        cn_pair_pow(key, (uint32_t)(t + T * j), trial, ST_CHAN, (uint32_t)a, p1, p2, c);
+        cn_pair_pow<kUni>(key, (uint32_t)(t + T * j), trial, ST_CHAN, (uint32_t)a, p1, p2, c);
         e2[SL::HALF + j] = p1;
         e2[SL::HALF + j + Q] = p2;
       }
@@ -473,7 +479,7 @@ struct Channel {
           int slot;
           pair_of(k, S, q, slot);
           R p1, p2;
-          cn_pair_pow(key, q, trial, ST_CHAN, (uint32_t)a, p1, p2, c);
+          cn_pair_pow<kUni>(key, q, trial, ST_CHAN, (uint32_t)a, p1, p2, c);
           e2[s] = slot == 0 ? p1 : p2;
         }
       }
@@ -579,7 +585,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   using CParams = const __attribute__((address_space(4))) TrialParams<R>;
   CParams& p = *(CParams*)(p0.points + pi);
   constexpr bool WAVEFFT = wave_fft_used(F, T, sizeof(R) == 8);
-  using FFT = std::conditional_t<WAVEFFT, WaveFft<F, T, R>, TeamFft<F, T, NBUF, R>>;
+  // CSI instances keep the stage-1 twiddles in global memory: their 4 KiB per-antenna power
+  // table plus the 1 KiB LDS copy would cross the 3-teams-per-CU line (LDS is allocated in
+  // 512-B granules: 54,368 B -> 54,784 B x 3 > 160 KiB; measured +10 % at 2 teams per CU).
+  using FFT = std::conditional_t<WAVEFFT, WaveFft<F, T, R, !CSI>, TeamFft<F, T, NBUF, R>>;
   using SL = Slots<F, T, NSLOT, ALIGNED>;
   using CHN = Channel<R, F, T, NSLOT, ALIGNED, CH>;
   constexpr int P = FFT::P;
@@ -592,10 +601,17 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   constexpr bool FREL = CSI;
 
   __shared__ C lds[FFT::LDS_TOTAL];
-  __shared__ R red[kMaxWaves];
-  __shared__ R vk_part[2][kMaxWaves];
+  __shared__ R red[T / 64];  // sized by the team
+  __shared__ R vk_part[2][T / 64];
   __shared__ R pw_csi[CSI ? kMaxCsiAnt : 1];  // per-antenna mean |H|^2 (CSI model)
   __shared__ C symw_s[SYMW_LDS ? NSLOT * T : 1];  // [slot][thread]
+  // wave-split FFT: stage 1 of the one-wave sub-transforms reads its twiddles from LDS
+  constexpr bool LTW1 = WAVEFFT && !CSI;
+  constexpr int TW1_N = [] {
+    if constexpr (LTW1) return FFT::TW1_N; else return 1;
+  }();
+  __shared__ C tw1_s[TW1_N];
+  const C* tw1 = LTW1 ? tw1_s : nullptr;
 
   const int t = threadIdx.x;
   const bool t0 = (t == 0);
@@ -616,8 +632,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   const R inv_sqrt_f = p.inv_sqrt_f;
   if constexpr (sizeof(R) == 8) {  // Box-Muller tables (real.h ln_unit / sincos_lut) into LDS
     for (int i = t; i < kLut64; i += T) lut64[i] = p.lut[i];
-    __syncthreads();
   }
+  if constexpr (LTW1) {  // the sub-transform's stage-1 twiddle block (offset 0 of tw_wave)
+    for (int i = t; i < TW1_N; i += T) tw1_s[i] = p.tw_wave[i];
+  }
+  if constexpr (sizeof(R) == 8 || LTW1) __syncthreads();
 
   // RX position for LoS / two-path (mp_model.py:190-201; y uses rx_loc_x, a reference quirk)
   double rx[3] = {0.0, 0.0, 0.0};
@@ -637,7 +656,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     for (int s = 0; s < NSLOT; ++s) {
       bool v;
       const int k = SL::k_of(s, tt, S, v);
-      lab_out[s] = v ? qam_label(key, k, trial, p.label_mask) : 0u;
+      lab_out[s] = v ? qam_label<CHN::kUni>(key, k, trial, p.label_mask) : 0u;
     }
   };
 #pragma unroll
@@ -724,6 +743,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // +0.8 %): symbols rebuilt from the labels per antenna, |Hhat|^2 recomputed after the FFT.
   // (every fp64 instance without symbols in LDS: F <= 2048 at 3 waves/SIMD, F 8192)
   constexpr bool SYMW_RE = !SYMW_LDS && sizeof(R) == 8;  // off: +13 % at F 8192
+  // Precode with w = 1 / ||Hhat|| / sqrt(F) folded into the channel first (vk then sums
+  // |Hhat w|^2 = vk / F): -1.1 % at F 2048 (wave-split instances); +5 % at F 4096, where
+  // the 16-point team's register allocation suffers (profiles/r03/ab_o/ab_paper.json).
+  constexpr bool PRE_EW = SYMW_RE && WAVEFFT;
   constexpr bool E2_RE = sizeof(R) == 8 && !SYMW_LDS;    // off: +2.8 % at F 8192 (ab_diet_prefetch.json)
   C symw_r[SYMW_LDS || SYMW_RE ? 1 : NSLOT];
   uint32_t slab_r[SYMW_RE ? NSLOT : 1];
@@ -815,9 +838,21 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
         const C e = hest(s);
-        x[s] = cmulc(symw(s), e);  // s conj(Hhat) / ||Hhat|| / sqrt(F); 0 off band (symw = 0)
-        e2[s] = fmar(e.x, e.x, e.y * e.y);
-        vk = fmar(e2[s], inv_nrm[s] * inv_nrm[s], vk);  // inv_nrm = 0 off band
+        if constexpr (PRE_EW) {
+          // the lattice point times conj(Hhat w), w = 1 / ||Hhat|| / sqrt(F): vk accumulates
+          // |Hhat w|^2 = |Hhat|^2 / ||Hhat||^2 / F directly (11 f64 ops per slot, not 13;
+          // vk_scale restores the factor F)
+          uint32_t l = slab_r[s];
+          R in = inv_nrm[s];
+          asm volatile("" : "+v"(l), "+v"(in));
+          const C ew = cscale(e, in * inv_sqrt_f);
+          x[s] = cmulc(levels_point<R>(l), ew);
+          vk = fmar(ew.x, ew.x, fmar(ew.y, ew.y, vk));
+        } else {
+          x[s] = cmulc(symw(s), e);  // s conj(Hhat) / ||Hhat|| / sqrt(F); 0 off band (symw = 0)
+          e2[s] = fmar(e.x, e.x, e.y * e.y);
+          vk = fmar(e2[s], inv_nrm[s] * inv_nrm[s], vk);  // inv_nrm = 0 off band
+        }
       }
       if (main_pass) {
         vk = wave_sum_lane63(vk);
@@ -825,9 +860,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       }
       SL::scatter(d, x, t0);
       if (!MIMO_ABL(p, ABL_FFT))
-        FFT::template run<+1, 0, SL::zero_mask()>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_ifft);
+        FFT::template run<+1, 0, SL::zero_mask()>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_ifft,
+                                                  tw1);
       if (!MIMO_ABL(p, ABL_PA)) pa_block(p.pa_kind, d, p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
-      if (!MIMO_ABL(p, ABL_FFT)) FFT::template run_second<-1>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_fft);
+      if (!MIMO_ABL(p, ABL_FFT))
+        FFT::template run_second<-1>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_fft, tw1);
       if constexpr (PIPE) {
         if (MIMO_ABL(p, ABL_FFT)) {  // no transforms ran, so no exchange windows (ABL_XCHG keeps them)
 #pragma unroll
@@ -837,10 +874,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       if (MIMO_ABL(p, ABL_FFT)) __syncthreads();  // keep the vk_part hand-off ordered
       R alpha_a = R(0);
       if (main_pass) {
-        R vks = R(0);
+        R vks = vk_part[a & 1][0];
 #pragma unroll
-        for (int i = 0; i < W; ++i) vks += vk_part[a & 1][i];
-        const R x = fmar(vks, p.inv_vk0, -R(1));
+        for (int i = 1; i < W; ++i) vks += vk_part[a & 1][i];
+        const R x = fmar(vks, PRE_EW ? p.inv_vk0_f : p.inv_vk0, -R(1));
         // Polynomial alpha: -7 % at F = 2048, but +3 % at F = 8192 (SGPR pressure of the
         // 8 waves/team instance, tools/ab_libs.py), so only up to F = 4096.
         if (sizeof(R) == 4 && F <= 4096 && absr(x) <= p.alpha_xlim) {
@@ -849,19 +886,20 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
           for (int i = 7; i >= 0; --i) acc = fmar(acc, x, p.apoly[i]);
           alpha_a = acc;
         } else if (sizeof(R) == 8 && absr(x) <= p.alpha_xlim) {
-          // Clenshaw: b_k = c_k + 2 t b_{k+1} - b_{k+2}; alpha = c_0 + t b_1 - b_2
-          // (~38 f64 ops instead of the library exp + erfc)
-          const double t2 = 2.0 * ((double)x / (double)p.alpha_xlim);
-          double b1 = 0.0, b2 = 0.0;
+          // Horner, 18 FMAs with the coefficients as SGPR operands instead of the library
+          // exp + erfc.  (Plain fma() compiles to v_fmac_f64 and copies every coefficient
+          // into the accumulator's VGPRs first, 2 v_mov per step: +0.7 % at F 2048, +0.9 %
+          // at F 4096, profiles/r03/ab_o.)
+          double acc = p.amono64[18];
 #pragma unroll
-          for (int k = 18; k >= 1; --k) {
-            const double b0 = fma(t2, b1, p.acheb[k] - b2);
-            b2 = b1;
-            b1 = b0;
+          for (int k = 17; k >= 0; --k) {
+            const double ck = p.amono64[k];
+            asm("v_fma_f64 %0, %1, %2, %3" : "=v"(acc) : "v"(acc), "v"((double)x), "s"(ck));
           }
-          alpha_a = (R)fma(0.5 * t2, b1, p.acheb[0] - b2);
+          alpha_a = (R)acc;
         } else {
-          alpha_a = alpha_of_gamma2(p.alpha_c / vks);
+          // (the register-diet pass sums vk / F: vks F is the precoding power)
+          alpha_a = alpha_of_gamma2(p.alpha_c / (PRE_EW ? vks * (R)F : vks));
         }
       }
 #pragma unroll
@@ -971,9 +1009,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       for (int s = 0; s < NSLOT; ++s)
         x[s] = ((valid_mask >> s) & 1u) ? cscale(qam_point<R>(lh[s], L, hb), inv_sqrt_f) : czero<R>();
       SL::scatter(d, x, t0);
-      FFT::template run<+1, 0, SL::zero_mask()>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t);
+      FFT::template run<+1, 0, SL::zero_mask()>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, false,
+                                                typename FFT::NoFill{}, tw1);
       pa_block(p.cnc_pa_kind, d, p.sat_cnc, p.sqrt_sat_cnc, p.inv_sat_cnc, p.rapp_p, p.toi_cnc);
-      FFT::template run_second<-1>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t);
+      FFT::template run_second<-1>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, false, typename FFT::NoFill{}, tw1);
       const R sc = inv_sqrt_f * p.inv_alpha_cnc;
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {

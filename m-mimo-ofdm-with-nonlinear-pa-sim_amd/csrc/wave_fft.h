@@ -51,7 +51,7 @@ constexpr int wave_fft_fw(int F, int T) { return F / (T / 64); }
 constexpr int wave_fft_tw_inter(int F, int T) { return fft_tw_total(wave_fft_fw(F, T), F / T); }
 constexpr int wave_fft_tw_total(int F, int T) { return wave_fft_tw_inter(F, T) + F; }
 
-template <int F, int T, typename Re>
+template <int F, int T, typename Re, bool LTW1 = true>
 struct WaveFft {
   using C = cx<Re>;
   static constexpr int P = F / T;
@@ -59,7 +59,8 @@ struct WaveFft {
   static constexpr int FW = F / WV;
   static constexpr int NB = P / WV;
   static_assert(wave_fft_ok(F, T), "wave-split plan needs >= 2 waves and P a multiple of the wave count");
-  using Sub = TeamFft<FW, 64, 1, Re, true>;
+  using Sub = TeamFft<FW, 64, 1, Re, true, LTW1>;  // LTW1: stage-1 twiddles from LDS (tw1)
+  static constexpr int TW1_N = Sub::TW1_N;         // tw1: a copy of the table's first TW1_N entries
   static_assert(Sub::P == P, "sub-transform keeps the points per thread");
   static constexpr int ROW = Sub::LDS_ELEMS;
   static constexpr int LDS_TOTAL = WV * ROW;
@@ -121,7 +122,8 @@ struct WaveFft {
   // Frequency (cyclic) -> time (wave k1, lane l, register m: n = k1 + WV (l + 64 m)).
   template <int DIR, int PAR = 0, uint32_t ZM = 0, typename Fill = NoFill>
   static __device__ __forceinline__ void run(C (&d)[P], C* lds, const C* __restrict__ tw, int t,
-                                             bool no_xchg = false, const Fill& fill = Fill{}) {
+                                             bool no_xchg = false, const Fill& fill = Fill{},
+                                             const C* tw1 = nullptr) {
     static_assert(DIR == +1, "run: the inverse (frequency -> time) transform");
     const C* twl = tw;
     int tl = t;
@@ -137,24 +139,29 @@ struct WaveFft {
     }
     fill(0);
     auto sub_fill = [&](int s) __attribute__((always_inline)) { fill(s + 1); };
-    Sub::template run<DIR, 0, 0u>(d, lds + w * ROW, twl, l, no_xchg, sub_fill);
+    Sub::template run<DIR, 0, 0u>(d, lds + w * ROW, twl, l, no_xchg, sub_fill, tw1);
   }
 
   // Time (as run() leaves it) -> frequency (cyclic).
   template <int DIR, typename Fill = NoFill>
   static __device__ __forceinline__ void run_second(C (&d)[P], C* lds, const C* __restrict__ tw, int t,
-                                                    bool no_xchg = false, const Fill& fill = Fill{}) {
+                                                    bool no_xchg = false, const Fill& fill = Fill{},
+                                                    const C* tw1 = nullptr) {
     static_assert(DIR == -1, "run_second: the forward (time -> frequency) transform");
     const C* twl = tw;
     int tl = t;
     asm volatile("" : "+s"(twl));
     asm volatile("" : "+v"(tl));
     const int w = tl >> 6, l = tl & 63;
-    Sub::template run<DIR, 0, 0u>(d, lds + w * ROW, twl, l, no_xchg, fill);
+    Sub::template run<DIR, 0, 0u>(d, lds + w * ROW, twl, l, no_xchg, fill, tw1);
     // B'[w, q] = B[w, q] e^{-j 2pi w q / F}, q = l + 64 m (wave-uniform branch)
+    // (all P loads issued before the first multiply: one wait instead of P round trips)
     if (w > 0) {
+      C tw[P];
 #pragma unroll
-      for (int m = 0; m < P; ++m) d[m] = cmul(d[m], Sub::gload(twl + TW_INTER, w * (l + 64 * m)));
+      for (int m = 0; m < P; ++m) tw[m] = Sub::gload(twl + TW_INTER, w * (l + 64 * m));
+#pragma unroll
+      for (int m = 0; m < P; ++m) d[m] = cmul(d[m], tw[m]);
     }
     if (!no_xchg) {
       C* wb = lds + w * ROW + l;
