@@ -261,6 +261,19 @@ __device__ __forceinline__ C pa_apply(int kind, C x, R sat, R sqrt_sat, R inv_sa
   return mkc(x.x * sc, x.y * sc);
 }
 
+// Cold paths out of line: the antenna loop's exact-alpha fallback (|x| > alpha_xlim) and
+// the general-hardness Rapp gain (library exp / erfc / log2 / exp2).  Inlined, their f64
+// constants were hoisted into the loop preheader and spilled to scratch once per trial
+// (~90 KB of writes per trial at config 2, profiles/r03/pmc); out of line they stay in
+// the call.  Measured: config 2 -2.5 %, CSI -2.7 %, LoS -2.3 %, two-path -3.0 %, F 8192
+// -0.4 %; F 4096 +1.6 %, so the 16-point F 4096 instance keeps them inline
+// (profiles/r03/ab_s/), as do the fp32 instances (not measured).
+__device__ __attribute__((noinline)) double alpha_of_gamma2_cold(double g2) { return alpha_of_gamma2(g2); }
+template <class C, typename R = real_of<C>>
+__device__ __attribute__((noinline)) C pa_rapp_general(C x, R inv_sat, R rapp_p) {
+  return pa_apply(PA_RAPP, x, R(0), R(0), inv_sat, rapp_p, R(0));
+}
+
 // y^(-1/N) for y >= 1 (the Rapp gain at integer hardness, N = 2p).  fp32: hardware
 // log / exp.  fp64: the fp32 hardware value z as the seed (~2^-22) and one third-order
 // step z (1 - e)^(-1/N) ~ z (1 + e/N + (N+1) e^2 / (2 N^2)), e = 1 - y z^N (error
@@ -297,7 +310,7 @@ __device__ __forceinline__ void rapp_int(C (&d)[P], R inv_sat) {
 }
 
 // PA on all P samples of a thread: one uniform branch on the kind, then a straight loop.
-template <int P, class C, typename R = real_of<C>>
+template <bool COLD_OUT, int P, class C, typename R = real_of<C>>
 __device__ __forceinline__ void pa_block(int kind, C (&d)[P], R sat, R sqrt_sat, R inv_sat, R rapp_p, R toi) {
 #ifdef MIMO_DIAG_PA_SOFTLIM_ONLY  // ISA inspection only (tools/one_inst.hip): no other PA kinds
   kind = PA_SOFTLIM;
@@ -311,7 +324,10 @@ __device__ __forceinline__ void pa_block(int kind, C (&d)[P], R sat, R sqrt_sat,
     rapp_int<2>(d, inv_sat);
   } else if (kind == PA_RAPP) {
 #pragma unroll
-    for (int m = 0; m < P; ++m) d[m] = pa_apply(PA_RAPP, d[m], sat, sqrt_sat, inv_sat, rapp_p, toi);
+    for (int m = 0; m < P; ++m) {
+      if constexpr (COLD_OUT) d[m] = pa_rapp_general(d[m], inv_sat, rapp_p);
+      else d[m] = pa_apply(PA_RAPP, d[m], sat, sqrt_sat, inv_sat, rapp_p, toi);
+    }
   } else if (kind == PA_TOI) {
 #pragma unroll
     for (int m = 0; m < P; ++m) d[m] = pa_apply(PA_TOI, d[m], sat, sqrt_sat, inv_sat, rapp_p, toi);
@@ -747,6 +763,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // |Hhat w|^2 = vk / F): -1.1 % at F 2048 (wave-split instances); +5 % at F 4096, where
   // the 16-point team's register allocation suffers (profiles/r03/ab_o/ab_paper.json).
   constexpr bool PRE_EW = SYMW_RE && WAVEFFT;
+  constexpr bool COLD_OUT = sizeof(R) == 8 && F != 4096;  // cold paths out of line (alpha_of_gamma2_cold)
   constexpr bool E2_RE = sizeof(R) == 8 && !SYMW_LDS;    // off: +2.8 % at F 8192 (ab_diet_prefetch.json)
   C symw_r[SYMW_LDS || SYMW_RE ? 1 : NSLOT];
   uint32_t slab_r[SYMW_RE ? NSLOT : 1];
@@ -862,7 +879,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       if (!MIMO_ABL(p, ABL_FFT))
         FFT::template run<+1, 0, SL::zero_mask()>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_ifft,
                                                   tw1);
-      if (!MIMO_ABL(p, ABL_PA)) pa_block(p.pa_kind, d, p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
+      if (!MIMO_ABL(p, ABL_PA)) pa_block<COLD_OUT>(p.pa_kind, d, p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
       if (!MIMO_ABL(p, ABL_FFT))
         FFT::template run_second<-1>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_fft, tw1);
       if constexpr (PIPE) {
@@ -899,7 +916,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
           alpha_a = (R)acc;
         } else {
           // (the register-diet pass sums vk / F: vks F is the precoding power)
-          alpha_a = alpha_of_gamma2(p.alpha_c / (PRE_EW ? vks * (R)F : vks));
+          const R g2 = p.alpha_c / (PRE_EW ? vks * (R)F : vks);
+          if constexpr (COLD_OUT) alpha_a = alpha_of_gamma2_cold(g2); else alpha_a = alpha_of_gamma2(g2);
         }
       }
 #pragma unroll
@@ -1011,7 +1029,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       SL::scatter(d, x, t0);
       FFT::template run<+1, 0, SL::zero_mask()>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, false,
                                                 typename FFT::NoFill{}, tw1);
-      pa_block(p.cnc_pa_kind, d, p.sat_cnc, p.sqrt_sat_cnc, p.inv_sat_cnc, p.rapp_p, p.toi_cnc);
+      pa_block<COLD_OUT>(p.cnc_pa_kind, d, p.sat_cnc, p.sqrt_sat_cnc, p.inv_sat_cnc, p.rapp_p, p.toi_cnc);
       FFT::template run_second<-1>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, false, typename FFT::NoFill{}, tw1);
       const R sc = inv_sqrt_f * p.inv_alpha_cnc;
 #pragma unroll
