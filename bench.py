@@ -188,7 +188,8 @@ def cpu_baseline(seconds=15.0, workload="2", iters=(0,), cores=None):
 
 def load_pmc_traffic(workload, iters, precision, trials_per_launch):
     """Per-launch HBM bytes from a committed rocprofv3 PMC summary of the SAME workload,
-    receiver iterations, precision and batch (tools/pmc_summary.py writes them)."""
+    receiver iterations, precision and batch (tools/pmc_traffic.py writes them).  Records of
+    an older kernel carry "superseded_by" and are skipped."""
     key = dict(workload=workload, iters=list(iters), precision=precision, trials_per_launch=trials_per_launch)
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "*pmc*.json"), recursive=True), reverse=True):
         try:
@@ -196,7 +197,7 @@ def load_pmc_traffic(workload, iters, precision, trials_per_launch):
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if all(d.get(k) == v for k, v in key.items()) and "hbm_bytes_per_launch" in d:
+        if all(d.get(k) == v for k, v in key.items()) and "hbm_bytes_per_launch" in d and "superseded_by" not in d:
             return d["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
     return None, None
 
