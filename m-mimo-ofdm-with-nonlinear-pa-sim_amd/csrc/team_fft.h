@@ -294,7 +294,7 @@ __device__ __forceinline__ void xchg_sync() {
 // LTW1: stage 1's twiddle block comes from an LDS copy (run()'s tw1 argument; the wave-split
 // FFT's one-wave sub-transforms, whose stage-1 block is small: 64 entries at F 2048) -- all
 // R - 1 twiddles read, none formed as products (fp64: 16 VALU ops per stage saved).
-template <int F, int T, int NBUF = 2, typename Re = float, bool WAVE = false, bool LTW1 = false>
+template <int F, int T, int NBUF = 2, typename Re = float, bool WAVE = false, bool LTW1 = false, bool LTW2_ON = false>
 struct TeamFft {
   using C = cx<Re>;
   static constexpr int P = F / T;
@@ -321,6 +321,19 @@ struct TeamFft {
   static constexpr int bits_before(int s) { return fft_bits_before(F, P, s); }
   // entries of stage 1's [R][NS] twiddle block (offset 0 of the table)
   static constexpr int TW1_N = NST > 1 ? (1 << fft_bits(F, P, 1)) * (1 << fft_bits_before(F, P, 1)) : 1;
+  // With LTW2_ON a radix-8 stage 2 also reads its non-power-of-two twiddles r = 3, 5, 6 from
+  // the LDS copy (rows [3][NS] after stage 1's block; r = 7 stays the product w4 w3): 3 of
+  // its 4 twiddle products per transform gone.  (All four rows would not fit next to the
+  // fp64 F 2048 team's 3-teams-per-CU LDS line.)
+  static constexpr bool LTW2 = LTW1 && LTW2_ON && NST >= 3 && fft_bits(F, P, 2) == 3;
+  static constexpr int NS2 = NST >= 3 ? 1 << fft_bits_before(F, P, 2) : 1;
+  static constexpr int TWL_N = TW1_N + (LTW2 ? 3 * NS2 : 0);  // entries of the LDS copy
+  // source index in the twiddle table of LDS-copy entry i < TWL_N
+  static __host__ __device__ constexpr int twl_src(int i) {
+    if (i < TW1_N) return i;
+    const int j = i - TW1_N, row = j / NS2, r = row == 0 ? 3 : row == 1 ? 5 : 6;
+    return fft_tw_off(F, P, 2) + r * NS2 + j % NS2;
+  }
   template <int S>
   static __host__ __device__ constexpr int pad(int e) { return e + (e >> psh(S)); }
   // Global-address-space load (the laundered table pointer would otherwise be generic
@@ -466,6 +479,8 @@ struct TeamFft {
       for (int r = 1; r < R; ++r) {
         if ((r & (r - 1)) == 0) {
           w0[r] = base.v[S][ilog2(r)];
+        } else if (LTW2 && S == 2 && r != 7) {
+          w0[r] = tw1[TW1_N + (r == 3 ? 0 : r == 5 ? 1 : 2) * NS + (t & (NS - 1))];
         } else {
           int hb = r;
           while (hb & (hb - 1)) hb &= hb - 1;

@@ -621,10 +621,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   __shared__ R vk_part[2][T / 64];
   __shared__ R pw_csi[CSI ? kMaxCsiAnt : 1];  // per-antenna mean |H|^2 (CSI model)
   __shared__ C symw_s[SYMW_LDS ? NSLOT * T : 1];  // [slot][thread]
-  // wave-split FFT: stage 1 of the one-wave sub-transforms reads its twiddles from LDS
+  // wave-split FFT: the one-wave sub-transforms read stage 1's twiddles and stage 2's rows
+  // r = 3, 5, 6 from LDS (team_fft.h TWL_N; -24 f64 ops per antenna at config 2)
   constexpr bool LTW1 = WAVEFFT && !CSI;
   constexpr int TW1_N = [] {
-    if constexpr (LTW1) return FFT::TW1_N; else return 1;
+    if constexpr (LTW1) return FFT::TWL_N; else return 1;
   }();
   __shared__ C tw1_s[TW1_N];
   const C* tw1 = LTW1 ? tw1_s : nullptr;
@@ -649,8 +650,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   if constexpr (sizeof(R) == 8) {  // Box-Muller tables (real.h ln_unit / sincos_lut) into LDS
     for (int i = t; i < kLut64; i += T) lut64[i] = p.lut[i];
   }
-  if constexpr (LTW1) {  // the sub-transform's stage-1 twiddle block (offset 0 of tw_wave)
-    for (int i = t; i < TW1_N; i += T) tw1_s[i] = p.tw_wave[i];
+  if constexpr (LTW1) {  // the sub-transform's stage-1 block and stage-2 rows (team_fft.h twl_src)
+    for (int i = t; i < TW1_N; i += T) tw1_s[i] = p.tw_wave[FFT::twl_src(i)];
   }
   if constexpr (sizeof(R) == 8 || LTW1) __syncthreads();
 

@@ -59,8 +59,13 @@ struct WaveFft {
   static constexpr int FW = F / WV;
   static constexpr int NB = P / WV;
   static_assert(wave_fft_ok(F, T), "wave-split plan needs >= 2 waves and P a multiple of the wave count");
-  using Sub = TeamFft<FW, 64, 1, Re, true, LTW1>;  // LTW1: stage-1 twiddles from LDS (tw1)
-  static constexpr int TW1_N = Sub::TW1_N;         // tw1: a copy of the table's first TW1_N entries
+  // LTW1: stage-1 twiddles from LDS (tw1); from four waves on (F 2048) also stage 2's rows
+  // r = 3, 5, 6 (config 2 -0.5 %, LoS -0.8 %, MCNC -1.0 %, profiles/r03/ab_x; at F 1024 the
+  // 3 KiB more would cost the third wave per SIMD)
+  using Sub = TeamFft<FW, 64, 1, Re, true, LTW1, LTW1 && (T / 64) >= 4>;
+  static constexpr int TW1_N = Sub::TW1_N;
+  static constexpr int TWL_N = Sub::TWL_N;         // tw1: LDS copy of the entries Sub::twl_src names
+  static __device__ __forceinline__ int twl_src(int i) { return Sub::twl_src(i); }
   static_assert(Sub::P == P, "sub-transform keeps the points per thread");
   static constexpr int ROW = Sub::LDS_ELEMS;
   static constexpr int LDS_TOTAL = WV * ROW;
