@@ -135,22 +135,24 @@ __device__ __forceinline__ double2 box_muller(uint32_t w0, uint32_t w1, double c
   return make_double2(rho * co, rho * s);
 }
 
+// sw: return the two draws swapped (z1 from words z, w); the swap selects the 32-bit words,
+// not the finished complex values (4 selects instead of 8 in float64).
 template <bool UNI = false, class C>
 __device__ __forceinline__ void cn_pair(Key key, uint32_t q, uint32_t trial, uint32_t stream, uint32_t aux, C& z1,
-                                        C& z2, real_of<C> c) {
+                                        C& z2, real_of<C> c, bool sw = false) {
   const uint4 w = philox4x32_10<UNI>(make_uint4(q, trial, stream, aux), key);
-  z1 = box_muller(w.x, w.y, c);
-  z2 = box_muller(w.z, w.w, c);
+  z1 = box_muller(sw ? w.z : w.x, sw ? w.w : w.y, c);
+  z2 = box_muller(sw ? w.x : w.z, sw ? w.y : w.w, c);
 }
 
 // |z1|^2, |z2|^2 of cn_pair's draws without forming them: rho^2 = c log(u1) (one log
 // per draw; no sqrt / sin / cos).  MRT norms only need the channel power.
 template <bool UNI = false, typename R>
 __device__ __forceinline__ void cn_pair_pow(Key key, uint32_t q, uint32_t trial, uint32_t stream, uint32_t aux, R& p1,
-                                            R& p2, R c) {
+                                            R& p2, R c, bool sw = false) {
   const uint4 w = philox4x32_10<UNI>(make_uint4(q, trial, stream, aux), key);
-  p1 = c * bm_log(w.x, R(0));
-  p2 = c * bm_log(w.z, R(0));
+  p1 = c * bm_log(sw ? w.z : w.x, R(0));
+  p2 = c * bm_log(sw ? w.x : w.z, R(0));
 }
 
 // Quarter pairing: sub-carrier k -> pair index q and slot (0: k1, 1: k2 = k1 + S/4).

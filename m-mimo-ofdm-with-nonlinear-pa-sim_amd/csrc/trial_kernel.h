@@ -149,8 +149,11 @@ struct Slots {
     for (int s = 0; s < NSLOT; ++s) {
       if constexpr (ALIGNED) {
         if (s == 0) {
-          d[0] = t0 ? czero<R>() : x[0];
-          d[HALF] = t0 ? x[0] : czero<R>();
+          // thread 0's slot 0 is bin S/2 (register HALF), the others' bin t (register 0):
+          // two multiplies by 0 / 1 per component instead of four 32-bit selects
+          const R m1 = t0 ? R(1) : R(0), m0 = R(1) - m1;
+          d[0] = cscale(x[0], m0);
+          d[HALF] = cscale(x[0], m1);
           continue;
         }
       }
@@ -411,9 +414,9 @@ struct Channel {
       for (int j = 0; j < Q; ++j) {
         C z1, z2;
         const bool sw = (j == 0) && t0;
-        cn_pair<kUni>(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, stream, aux, z1, z2, c);
-        z[j] = sw ? z2 : z1;
-        z[j + Q] = sw ? z1 : z2;
+        cn_pair<kUni>(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, stream, aux, z1, z2, c, sw);
+        z[j] = z1;
+        z[j + Q] = z2;
         cn_pair<kUni>(key, (uint32_t)(t + T * j), trial, stream, aux, z1, z2, c);
         z[SL::HALF + j] = z1;
         z[SL::HALF + j + Q] = z2;
@@ -449,9 +452,9 @@ struct Channel {
       if ((c & 1) == 0) {
         const bool sw = (j == 0) && (t == 0);
         cn_pair<kUni>(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)((S >> 2) - 1 + t + T * j), trial, stream, aux, z1, z2,
-                cs);
-        z[j] = sw ? z2 : z1;
-        z[j + Q] = sw ? z1 : z2;
+                cs, sw);
+        z[j] = z1;
+        z[j + Q] = z2;
       } else {
         cn_pair<kUni>(key, (uint32_t)(t + T * j), trial, stream, aux, z1, z2, cs);
         z[SL::HALF + j] = z1;
@@ -477,9 +480,9 @@ struct Channel {
         R p1, p2;
         const bool sw = (j == 0) && t0;
         cn_pair_pow<kUni>(key, sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, ST_CHAN, (uint32_t)a, p1, p2,
-                    c);
-        e2[j] = sw ? p2 : p1;
-        e2[j + Q] = sw ? p1 : p2;
+                    c, sw);
+        e2[j] = p1;
+        e2[j + Q] = p2;
         cn_pair_pow<kUni>(key, (uint32_t)(t + T * j), trial, ST_CHAN, (uint32_t)a, p1, p2, c);
         e2[SL::HALF + j] = p1;
         e2[SL::HALF + j + Q] = p2;
