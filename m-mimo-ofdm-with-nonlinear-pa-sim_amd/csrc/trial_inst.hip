@@ -22,15 +22,15 @@ constexpr bool kF64 = INST_F64 != 0;
 using Real = std::conditional_t<kF64, double, float>;
 
 // Occupancy profile per instance (see trial_kernel): waves/SIMD target, exchange buffers,
-// symbols in LDS.  Measured on MI355X (tools/ab_libs.py, profiles/r01/ab_*.json):
-//  - fp64 below F = 8192: 2 waves/SIMD (255 VGPRs), one exchange buffer, the weighted
-//    symbols in LDS (F = 2048: 65 KiB / team, 2 teams per CU).
-//  - aligned, 16 points/thread, F <= 4096: 3 waves/SIMD needs <= 168 VGPRs and
-//    <= 160 KiB / (3 waves x 4 SIMD / waves per team) of LDS -> one exchange buffer and
-//    the weighted symbols in LDS (F = 2048: 25 KiB / team).  (Two-path at 2 waves/SIMD
-//    measured 12 % slower.)
-//  - aligned, 8 points/thread: 4 waves/SIMD fit in 128 VGPRs with two buffers.
-//  - generic (unaligned band), 16 slots/thread: symbols in LDS to limit spills.
+// symbols in LDS.  Measured on MI355X (tools/ab_libs.py; DESIGN.md §3 has the A/Bs):
+//  - fp64 up to F = 2048: 3 waves/SIMD (<= 168 VGPRs), one exchange buffer, the symbols
+//    rebuilt per antenna from packed lattice levels (no symbols in LDS), 3 teams per CU.
+//  - fp64 F = 4096: the 256-thread 16-point team, 2 waves/SIMD, one buffer, 2 teams/CU.
+//  - fp64 F = 8192: the 512-thread 16-point team, 2 waves/SIMD, one team per CU.
+//  - fp32 aligned, 16 points/thread, F <= 4096: 3 waves/SIMD with one exchange buffer and
+//    the weighted symbols in LDS (F = 2048: 25 KiB / team).
+//  - fp32 aligned, 8 points/thread: 4 waves/SIMD fit in 128 VGPRs with two buffers.
+//  - generic (unaligned band): symbols in LDS to limit spills.
 struct Profile {
   int minw, nbuf;
   bool symw_lds;
@@ -40,8 +40,7 @@ constexpr Profile profile_for(int T, bool aligned, int ch) {
   if (kF64 && kF >= 8192) return Profile{2, 1, false};  // 136 KiB exchange buffer: one team per CU (T = 512: 2 waves/SIMD)
   // fp64 up to F 2048: 3 waves/SIMD (168 VGPRs; the symbols rebuilt from the labels and
   // |Hhat|^2 after the FFT, so 49.5 KiB of LDS per 256-thread team and 3 teams per CU):
-  // -8.5 % at config 2 (profiles/r03/ab_w3/).  F 4096 (8-wave teams, 84 KiB) cannot host a
-  // second team, so it stays at 2 waves/SIMD with the symbols in LDS.
+  // -8.5 % at config 2 (profiles/r03/ab_w3/).
   if (kF64 && kF <= 2048) return Profile{3, 1, false};
   if (kF64 && kF == 4096) return Profile{2, 1, false};  // 16-point team, symbols from levels: 2 teams/CU
   if (kF64) return Profile{2, 1, true};

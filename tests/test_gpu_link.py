@@ -133,14 +133,23 @@ def test_published_curve_paper_config(receiver, channel):
     leave room for another seed's sampling: >= 50 % within 1 sigma, >= 85 % within 2, mean
     z^2 <= 1.8, max |z| <= 4.5.  (The reference's workers replay one Rayleigh sequence,
     channel.py:209-212: emulating that with 4-32 workers changed none of these numbers by
-    more than sampling noise, so the replicas draw independent channels.)"""
+    more than sampling noise, so the replicas draw independent channels.)
+
+    The z statistics alone would pass a small bias shared by every point (the replica sigma
+    is ~3x the engine's), so the bias bounds stay as well: on the compared points the median
+    |relative difference| <= 3 % and, per counter row with >= 3 compared points, the mean
+    relative difference within +-2 % (round-4 record: profiles/r04/)."""
     import replay_sigma
     out, _ = replay_sigma.measure(receiver, channel, workers=(1,), reps=24)
     st = out["by_workers"]["1"]
-    print(receiver, channel, out["compared"], st)
+    print(receiver, channel, out["compared"], st, "median |rel|", out["median_abs_rel"], "row mean rel",
+          out["row_mean_rel"])
     assert out["compared"] >= 60
     assert st["frac_abs_z_le1"] >= 0.5 and st["frac_abs_z_le2"] >= 0.85
     assert st["mean_z2"] <= 1.8 and st["max_abs_z"] <= 4.5
+    assert out["median_abs_rel"] <= 0.03
+    for row, bias in out["row_mean_rel"].items():
+        assert abs(bias) <= 0.02, (row, bias)
 
 
 def test_sixteen_workers_share_two_engines(tmp_path, monkeypatch):

@@ -22,9 +22,13 @@ CFG2 = dict(n_ant=64, n_sc=1024, n_fft=2048, constel_size=64, pa="softlim", ibo_
 N_TRIALS = 4096
 ITERS = [0, 1, 2]
 # Lower bounds on the fraction of (trial, counter) entries where f32 == f64, per Eb/N0.
-# 1000 dB: 1-3 differing entries of 16,384 (0.99994 in round 2, 0.99982 after the round-3
-# FFT rounding changes): the bound allows 8.
-MIN_AGREE = {15.0: 0.999, 30.0: 0.999, 1000.0: 0.9995}  # measured 0.99939, 0.99957, 0.99982
+# 1000 dB (no noise: a decision flips only where the clipped signal sits within fp32
+# rounding of a slicer boundary): 1 differing entry of 16,384 in round 2 (0.99994); 3 after
+# round 3's FFT rounding changes (0.99982, the W8 / W16 rotations folded into FMAs change
+# the rounding of both instances); 5 at the round-3 final record (0.999695,
+# profiles/r03/check_z/pytest_gpu.log).  The bound allows 8 entries: a margin of 3 over the
+# last record, since every rounding-order change in either instance moves this count.
+MIN_AGREE = {15.0: 0.999, 30.0: 0.999, 1000.0: 0.9995}  # measured (r03 final) ~0.9994, ~0.9996, 0.999695
 
 
 @pytest.mark.parametrize("ebn0", [15.0, 30.0, 1000.0])

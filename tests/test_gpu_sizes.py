@@ -70,7 +70,8 @@ CONFIG5 = [
 def test_config5_array_vs_oracle(A, M, pa, p, ibo, channel, receiver, n, prec):
     """BASELINE config 5's array at one user (256 antennas, F 8192, 4096 sub-carriers,
     Rapp p = 3) and the other F 8192 receivers / channels: per-trial counts EXACTLY equal to
-    the oracle's (the fp64 instance runs the pair-wave FFT and block state memory)."""
+    the oracle's.  The fp64 instance is the 512-thread team (T = 512, 16 points per thread,
+    radix 8.8.8.16 TeamFft, per-slot state in registers), as eng.describe() prints."""
     F, S = 8192, 4096
     snr = float(sim.rm.ebn0_to_snr(15.0, S, S, M))
     cfg = sim.SimConfig(A, S, F, M, pa=pa, p_hardness=p, ibo_db=ibo, snr_db=snr, channel=channel, receiver=receiver)

@@ -81,8 +81,12 @@ def measure(receiver, channel, workers=(1, 4, 8, 16, 32), reps=24, n_tr=8192):
     # n_err_min errors or the bit budget)
     n_ref = np.minimum(BITS_MAX / BPS, np.ceil(N_ERR_MIN / np.maximum(pub, 1e-300) / BPS).max(axis=0)).astype(int)
     sel = pub >= 1e-4
+    # bias view (independent of sigma): relative difference per compared point, its median
+    # magnitude, and its mean per counter row (rows with >= 3 compared points)
+    rel = (ber - pub) / np.where(sel, pub, 1.0)
+    row_bias = {str(r): round(float(rel[r][sel[r]].mean()), 5) for r in range(len(pub)) if sel[r].sum() >= 3}
     out = dict(receiver=receiver, channel=channel, n_tr=n_tr, reps=reps, n_ref=n_ref.tolist(), compared=int(sel.sum()),
-               by_workers={})
+               median_abs_rel=round(float(np.median(np.abs(rel[sel]))), 5), row_mean_rel=row_bias, by_workers={})
     for W in workers:
         sig_ref = np.zeros_like(pub)
         engines = {}
