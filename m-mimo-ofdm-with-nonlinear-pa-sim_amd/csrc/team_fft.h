@@ -313,7 +313,22 @@ struct TeamFft {
   // (fp64 F 4096 on 256 threads: 1/32, so that two teams fit a CU -- 80,256 B each)
   static constexpr int PAD0 = (sizeof(Re) == 8 && F < 8192) ? (F == 4096 && T == 256 ? 5 : 3) : 4;
   static constexpr int psh(int S) { return S == 0 ? PAD0 : PADN; }
-  static constexpr int LDS_ELEMS = F + F / (1 << (PAD0 < PADN ? PAD0 : PADN));
+  // Exchange 0 transposed (XP0): stage 0 (NS = 1) writes element e = R0 j + r, which the
+  // linear layouts above put R0 elements apart in consecutive lanes (an R0-element stride
+  // is a multiple of the 8 x 16-B bank groups of ds_write_b128: 8-way conflicts unpadded,
+  // 2-way at 1/16, 1/8 of the buffer to remove them).  Stored as [R0][F / R0 + XD0]
+  // (address (e % R0) XS0 + e / R0) the writes of one r are consecutive in the lanes and
+  // stage 1's reads (e = t + T m) land on 16 distinct 16-B bank groups per read group:
+  // conflict-free for XD0 = 32 / R0 (R0 = 4: 4 in fp64, 8 in fp32) in both precisions
+  // (tools/lds_conflicts.py --xpose, tests/test_lds_layout.py), for R0 XD0 <= 32 extra
+  // elements instead of F / 16.
+  static constexpr int R0 = NST > 1 ? 1 << fft_bits(F, P, 0) : 1;
+  static constexpr bool XP0 = NST > 1 && R0 >= 4 && R0 <= 16 && T % R0 == 0;
+  static constexpr int XD0 = !XP0 ? 0 : R0 == 4 ? (sizeof(Re) == 8 ? 4 : 8) : 32 / R0;
+  static constexpr int XS0 = F / R0 + XD0;  // row stride of the transposed exchange 0
+  static constexpr int lin_elems(int sh) { return F + F / (1 << sh); }
+  static constexpr int LDS_ELEMS = XP0 ? (R0 * XS0 > lin_elems(PADN) ? R0 * XS0 : lin_elems(PADN))
+                                       : lin_elems(PAD0 < PADN ? PAD0 : PADN);
   static_assert((1 << LOG_F) == F && (1 << LOG_P) == P && P >= 2, "power-of-two sizes");
   static_assert(!WAVE || T == 64, "wave-local transforms are one wave");
 
@@ -399,11 +414,18 @@ struct TeamFft {
       // overwritten.  The barrier sits after this stage's twiddle loads and DFT, so
       // their latency overlaps the previous exchange's reads.
       if constexpr (NBUF == 1 && I == 0) xchg_sync<WAVE>();
-      // pad(base + r NS) == pad(base) + pad(r NS) for power-of-two NS, R, T (the
-      // padding never splits a write group): one address per i, immediate offsets.
-      C* wb = buf + pad<S>((j / NS) * NS * R + jm);
+      if constexpr (S == 0 && XP0) {
+        // transposed exchange 0: element R j + r at r XS0 + j
+        C* wb = buf + j;
 #pragma unroll
-      for (int r = 0; r < R; ++r) wb[pad<S>(r * NS)] = v[r];
+        for (int r = 0; r < R; ++r) wb[r * XS0] = v[r];
+      } else {
+        // pad(base + r NS) == pad(base) + pad(r NS) for power-of-two NS, R, T (the
+        // padding never splits a write group): one address per i, immediate offsets.
+        C* wb = buf + pad<S>((j / NS) * NS * R + jm);
+#pragma unroll
+        for (int r = 0; r < R; ++r) wb[pad<S>(r * NS)] = v[r];
+      }
     }
   }
 
@@ -506,9 +528,16 @@ struct TeamFft {
     if constexpr (!LAST) {
       if (!no_xchg) {
         xchg_sync<WAVE>();
-        const C* rb = buf + pad<S>(t);
+        if constexpr (S == 0 && XP0) {
+          // element t + T m at (t % R0) XS0 + t / R0 + (T / R0) m
+          const C* rb = buf + (t % R0) * XS0 + t / R0;
 #pragma unroll
-        for (int m = 0; m < P; ++m) d[m] = rb[pad<S>(T * m)];
+          for (int m = 0; m < P; ++m) d[m] = rb[(T / R0) * m];
+        } else {
+          const C* rb = buf + pad<S>(t);
+#pragma unroll
+          for (int m = 0; m < P; ++m) d[m] = rb[pad<S>(T * m)];
+        }
       }
       // Independent caller work placed between this exchange's reads and their first use
       // (same basic block: the scheduler interleaves it with the LDS latency).

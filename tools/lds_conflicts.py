@@ -14,6 +14,7 @@ candidate per-exchange layouts e -> e + (e >> k) * q (padding: keeps the immedia
 addressing of team_fft.h valid when it never splits a write group).
 
     python tools/lds_conflicts.py            # both precisions, the production team sizes
+    python tools/lds_conflicts.py --xpose    # + exchange 0 in team_fft.h's transposed layout
 """
 import itertools
 import sys
@@ -87,6 +88,26 @@ def exchange_cost(F, T, s, layout, dw):
     return extra
 
 
+def xpose_layout(F, T, dw):
+    """team_fft.h XP0: exchange 0 stored as [R0][F / R0 + 32 / R0]."""
+    R0 = stages(F, T)[1][0][0]
+    xs = F // R0 + (32 // R0 if R0 > 4 else (4 if dw == 4 else 8))
+    return lambda e: (e % R0) * xs + e // R0
+
+
+def production_costs(F, T, dw, padn=5):
+    """Extra cycles per transform of every exchange in the production layout (XP0 for
+    exchange 0 when R0 >= 4, 1/2^padn linear padding after)."""
+    P, st = stages(F, T)
+    out = []
+    for s in range(len(st) - 1):
+        if s == 0 and 4 <= st[0][0] <= 16 and T % st[0][0] == 0:
+            out.append(exchange_cost(F, T, 0, xpose_layout(F, T, dw), dw))
+        else:
+            out.append(exchange_cost(F, T, s, lambda e: e + (e >> padn), dw))
+    return out
+
+
 def linear_ok(F, T, s, k, q):
     """pad(base + r NS) == pad(base) + pad(r NS) for every write of exchange s."""
     P, st = stages(F, T)
@@ -121,8 +142,14 @@ def best_pads(F, T, dw, ks=range(2, 8), qs=(1, 2, 3)):
 if __name__ == "__main__":
     cfgs = [(2, 2048, 128), (2, 4096, 256), (2, 8192, 512),
             (4, 512, 64), (4, 1024, 128), (4, 2048, 256), (4, 4096, 512), (4, 8192, 512)]
+    xp = "--xpose" in sys.argv
+    sizes = [a for a in sys.argv[1:] if a.isdigit()]
     for dw, F, T in cfgs:
-        if len(sys.argv) > 1 and str(F) not in sys.argv[1:]:
+        if sizes and str(F) not in sizes:
+            continue
+        if xp:
+            print(f"{'f32' if dw == 2 else 'f64'} F={F} T={T} production (XP0 + 1/32) extra per exchange: "
+                  f"{production_costs(F, T, dw)}")
             continue
         print(f"{'f32' if dw == 2 else 'f64'} F={F} T={T} stages={stages(F, T)[1]}")
         for s, rs, cands, cur in best_pads(F, T, dw):
