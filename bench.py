@@ -9,6 +9,9 @@ under torchrun; without an outer torchrun the script starts it as a child proces
 shards trials by index: weak scaling, no data-path collective; the per-step error counts
 are summed across ranks once at the end (RCCL all_reduce).
 
+After the headline's timed region the same ranks time north_star's own split, BASELINE
+config 4's 915-point SNR x IBO grid dealt over them (``grid`` object; ``--no-grid`` skips it).
+
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
@@ -222,6 +225,58 @@ def launch_ranks(n):
     return proc.returncode
 
 
+def time_grid(rank, world, dist, dev, precision, tdev, fake=False):
+    """North_star's multi-GPU split (BASELINE config 4): ``sweep.run_grid`` over the 915-point
+    SNR x IBO extent (sweep.BASELINE_C4), grid points dealt over the N ranks by estimated cost
+    (LPT), one all-reduce of the counters -- exactly what the reference's fixed-BER driver runs
+    point by point on one host (main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:100-215).
+    Strong scaling: the grid is fixed, N ranks share it.  Timed between barriers after an
+    untimed engine set-up; the wall time is the MAX over ranks.  ``fake``: the CPU rehearsal
+    (tests/fake_link.py stand-in, no GPU) of the same plumbing."""
+    import hashlib
+
+    import sweep
+    c4 = sweep.BASELINE_C4
+    if fake:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from fake_link import FakeLink
+        link = FakeLink()
+    else:
+        link = sweep.paper_link("rayleigh", "cnc", precision, device=dev, n_err_min=c4["n_err_min"],
+                                bits_sent_max=c4["bits_sent_max"])
+        link.engine().run(0, 0, 1, [0])  # engine / device set-up outside the timed region
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    err, bits = sweep.run_grid(link, c4["ibo"], c4["ebn0"], c4["iters"], incl_clean=False, seed=2137, rank=rank,
+                               world=world, dist=dist, device=dev)
+    if not fake:
+        import torch
+        torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ranks = 1
+    if dist:
+        import torch
+        t = torch.tensor([dt, 1.0], device=tdev, dtype=torch.float64)
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:])
+        dt, ranks = float(t[0].item()), int(t[1].item())
+    m = link.my_mod
+    bits_per_sym = int(m.n_sub_carr * np.log2(m.constel_size))
+    n_sym = int(bits[..., 0].sum()) // bits_per_sym
+    digest = hashlib.sha256(np.ascontiguousarray(err, np.int64).tobytes() +
+                            np.ascontiguousarray(bits, np.int64).tobytes()).hexdigest()[:16]
+    return {"workload": "BASELINE config 4: Eb/N0 0-30 dB x IBO 0-7 dB (0.5 dB steps), CNC iterations 0-8, "
+                        "bits_sent_max 5e6 / n_err_min 1e5 per point, 64-ant / FFT 4096 / 2048-sc paper geometry"
+                        + (" [CPU rehearsal: stand-in link]" if fake else ""),
+            "points": int(len(c4["ibo"]) * len(c4["ebn0"])), "ofdm_symbols": n_sym, "wall_s": round(dt, 4),
+            "symbols_per_s": round(n_sym / dt, 1), "ranks_seen": ranks, "scaling": "strong",
+            "parallelism": f"points dealt by cost (LPT) over {world} rank(s), one all-reduce of the counters",
+            "counts_digest": digest}
+
+
 def check_launch(world, rank):
     """``--check-launch``: the rank plumbing only (process group over gloo, the world size
     the driver asked for, one all_reduce); no engine, no GPU.  For the CPU launcher test."""
@@ -249,6 +304,8 @@ def main():
     ap.add_argument("--workload", default="2", choices=sorted(WORKLOADS),
                     help="2 = BASELINE config 2 (headline); paper; 5su (config-5 array, one user)")
     ap.add_argument("--check-launch", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-grid", action="store_true", help="skip the config-4 grid line (the 'grid' object)")
+    ap.add_argument("--grid-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -261,6 +318,18 @@ def main():
         sys.exit(2)
     if args.check_launch:
         return check_launch(world, rank)
+    if args.grid_check:  # CPU rehearsal of the grid line: gloo ranks, stand-in link, no GPU
+        import torch.distributed as gdist
+        gd = None
+        if world > 1:
+            gdist.init_process_group("gloo")
+            gd = gdist
+        g = time_grid(rank, world, gd, None, args.precision, "cpu", fake=True)
+        if gd:
+            gd.destroy_process_group()
+        if rank == 0:
+            print(json.dumps({"check": "grid", "n_gpus": world, "grid": g}), flush=True)
+        return
     import torch
     dist = None
     # MIMO_BENCH_BACKEND=gloo rehearses the N > 1 path with ranks sharing the visible GPUs
@@ -350,6 +419,8 @@ def main():
                         "trials; the fused kernel does not move them (a model figure, not traffic)"},
         "ber": [round(float(x) / (total_trials * wl["S"] * np.log2(wl["M"])), 8) for x in err_tot],
     }
+    if not args.no_grid and args.workload == "2" and args.precision == "f64":
+        out["grid"] = time_grid(rank, world, dist, dev, args.precision, tdev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.workload, iters)
     if dist:

@@ -18,6 +18,7 @@
  *     mimo_ofdm_tx / _rx        <- _tx_ofdm_symbol / _rx_ofdm_symbol   modulation.py:248-293
  *     mimo_fft                  <- utilities.to_freq/time_domain       utilities.py:311-339
  *     mimo_pa                   <- SoftLimiter/Rapp/ThirdOrderNonLin.process  distortion.py
+ *     mimo_calc_alpha           <- Modem.calc_alpha                    modulation.py:178-189
  *     mimo_mrt_precode          <- AntennaArray.set_precoding_matrix   antenna_array.py:162-185
  *     mimo_combine              <- Miso*Fd.propagate                   channel.py:74-89,277-292
  *     mimo_awgn                 <- Awgn.process                        noise.py:45-83
@@ -39,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MIMO_ABI_VERSION 5
+#define MIMO_ABI_VERSION 6
 
 enum { MIMO_OK = 0, MIMO_EINVAL = -1, MIMO_EHIP = -2, MIMO_ENOKERNEL = -3, MIMO_ENOMEM = -4 };
 enum { MIMO_PA_NONE = 0, MIMO_PA_SOFTLIM = 1, MIMO_PA_RAPP = 2, MIMO_PA_TOI = 3 };
@@ -75,6 +76,11 @@ typedef struct mimo_config {
                                replay one seeded channel sequence (channel.py:209-212);
                                bits and noise stay per trial.  Used to size the published
                                curves' channel variance (tests/test_gpu_link.py).  (ABI 5) */
+  uint64_t csi_seed;        /* MIMO_CH_TABLE with CSI error: Philox key of the one erroneous
+                               estimate every trial and every run shares -- Link.__init__ draws it
+                               once from its own CSI noise generator (mp_model.py:76-87), so the
+                               workers of a point see the same estimate whatever their seeds.
+                               0: the run's seed (ABI 5 behaviour).  (ABI 6) */
 } mimo_config;
 
 /* Grid-point parameters: what Link keeps in its PA / receiver / noise objects. */
@@ -137,6 +143,9 @@ int32_t mimo_ofdm_rx(int32_t n_fft, int32_t n_sub_carr, int32_t cp_len, int64_t 
                      double* sym_iq);
 int32_t mimo_pa(int32_t kind, double sat_pow, double p_hardness, double toi_coeff, const double* in_iq, int64_t n,
                 double* out_iq);
+/* Bussgang gain alpha(IBO) for n IBO values [dB], by the trial kernel's segment table
+ * (alpha_fit.h: the float64 kernels' alpha for antennas outside the per-point fit).  (ABI 6) */
+int32_t mimo_calc_alpha(const double* ibo_db, int64_t n, double* out);
 int32_t mimo_mrt_precode(int32_t n_ant, int32_t n_cols, const double* h_iq, double* p_iq);
 int32_t mimo_combine(int32_t n_ant, int64_t n, const double* h_iq, const double* y_iq, double* out_iq);
 int32_t mimo_awgn(uint64_t seed, uint64_t counter, int64_t n, double noise_std, const double* in_iq, double* out_iq);

@@ -40,7 +40,8 @@ class MimoConfig(ctypes.Structure):
                 ("constel_size", ctypes.c_int32), ("cp_len", ctypes.c_int32), ("channel_kind", ctypes.c_int32),
                 ("receiver_kind", ctypes.c_int32), ("device", ctypes.c_int32), ("rx_pos", ctypes.c_double * 3),
                 ("rx_loc_var", ctypes.c_double), ("reroll_chan", ctypes.c_int32), ("precision", ctypes.c_int32),
-                ("tx_pos", _dp), ("carrier_freqs", _dp), ("chan_table", _dp), ("chan_replay_period", ctypes.c_int32)]
+                ("tx_pos", _dp), ("carrier_freqs", _dp), ("chan_table", _dp), ("chan_replay_period", ctypes.c_int32),
+                ("csi_seed", ctypes.c_uint64)]
 
 
 class MimoPoint(ctypes.Structure):
@@ -72,6 +73,7 @@ SYMBOLS = {
     "mimo_ofdm_rx": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, _dp, _dp]),
     "mimo_pa": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_double, _dp,
                                  ctypes.c_int64, _dp]),
+    "mimo_calc_alpha": (ctypes.c_int32, [_dp, ctypes.c_int64, _dp]),
     "mimo_mrt_precode": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, _dp, _dp]),
     "mimo_combine": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int64, _dp, _dp, _dp]),
     "mimo_awgn": (ctypes.c_int32, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, ctypes.c_double, _dp, _dp]),
@@ -127,7 +129,7 @@ class Engine:
 
     def __init__(self, n_ant, n_sub_carr, n_fft, constel_size, cp_len, channel, receiver, tx_pos, rx_pos,
                  rx_loc_var, carrier_freqs, reroll=True, device=-1, precision=None, chan_table=None,
-                 chan_replay_period=0):
+                 chan_replay_period=0, csi_seed=0):
         L = lib()
         self.precision = precision or default_precision()
         if self.precision not in PRECISIONS:
@@ -148,7 +150,7 @@ class Engine:
                          precision=PRECISIONS[self.precision],
                          tx_pos=_ptr(self._tx, ctypes.c_double), carrier_freqs=_ptr(self._fr, ctypes.c_double),
                          chan_table=_ptr(self._tab, ctypes.c_double) if self._tab is not None else None,
-                         chan_replay_period=int(chan_replay_period))
+                         chan_replay_period=int(chan_replay_period), csi_seed=int(csi_seed))
         cfg.rx_pos[:] = [float(v) for v in rx_pos]
         h = L.mimo_engine_create(ctypes.byref(cfg))
         if not h:
@@ -294,6 +296,14 @@ def pa(kind, x, sat_pow=0.0, p_hardness=0.0, toi_coeff=0.0):
                          _ptr(out.view(np.float64), ctypes.c_double)))
     out = out.reshape(x2.shape)
     return out.real.copy() if is_real else out
+
+
+def calc_alpha(ibo_db):
+    """Bussgang gain per IBO [dB] by the float64 kernels' segment table (alpha_fit.h)."""
+    ibo = np.ascontiguousarray(np.atleast_1d(np.asarray(ibo_db, np.float64)))
+    out = np.empty(ibo.size, np.float64)
+    _check(lib().mimo_calc_alpha(_ptr(ibo, ctypes.c_double), ibo.size, _ptr(out, ctypes.c_double)))
+    return out.reshape(np.shape(ibo_db))
 
 
 def mrt_precode(h_sc):

@@ -136,9 +136,17 @@ AlphaFit fit_alpha(double g0sq) {
   return p;
 }
 
-// fp64 Box-Muller tables (real.h ln_unit / sincos_lut), computed in long double.
+// fp64 Box-Muller tables (real.h ln_unit / sincos_lut), computed in long double, followed
+// by the Bussgang-gain segment table (alpha_fit.h; stays in HBM, the kernel copies only the
+// first kLut64 entries into LDS).
+constexpr int kLut64Alloc = mimo::kLut64 + (mimo::kAlphaTabDoubles + 1) / 2;
 std::vector<double2> lut64_table() {
-  std::vector<double2> t(mimo::kLut64);
+  std::vector<double2> t(kLut64Alloc);
+  {
+    const std::vector<double> at = mimo::alpha_segment_table();
+    double* dst = reinterpret_cast<double*>(t.data() + mimo::kLut64);
+    for (int i = 0; i < mimo::kAlphaTabDoubles; ++i) dst[i] = at[i];
+  }
   {  // real.h ln_unit: bucket i = m in [0.5 + i 2^-10, 0.5 + (i + 1) 2^-10), c = 1 for the top one
     for (int i = 0; i < mimo::kLnTab; ++i) {
       double c = 1.0;
@@ -321,6 +329,7 @@ void fill_point(mimo_engine* e, const mimo_point& pt, uint64_t seed, uint64_t fi
   const mimo_config& c = e->cfg;
   const bool csi = pt.csi_eps >= 0;
   p.seed = seed;
+  p.csi_seed = c.csi_seed ? c.csi_seed : seed;  // used by CH_TABLE + CSI only
   p.first_trial = first_trial;
   p.pa_kind = pt.pa_kind;
   p.cnc_pa_kind = pt.cnc_pa_kind;

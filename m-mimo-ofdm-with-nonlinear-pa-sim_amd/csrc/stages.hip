@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../include/mimo_engine.h"
+#include "alpha_fit.h"
 #include "philox.h"
 
 namespace {
@@ -354,6 +355,33 @@ int32_t mimo_pa(int32_t kind, double sat, double p, double toi, const double* in
   hipLaunchKernelGGL(k_pa, grid_for(n), dim3(256), 0, 0, kind, sat, p, toi, din.as<double2>(), n, dout.as<double2>());
   S_TRY(hipGetLastError());
   S_TRY(hipMemcpy(out_iq, dout.p, n * sizeof(double2), hipMemcpyDeviceToHost));
+  return MIMO_OK;
+}
+
+// Modem.calc_alpha (modulation.py:178-189) through the trial kernel's segment table
+// (alpha_fit.h alpha_seg).  alpha_seg wants a wave-uniform argument (scalar coefficient
+// loads): one wave per element.
+__global__ void k_calc_alpha(const double* g2, const double* tab, double* out) {
+  const double a = mimo::alpha_seg(g2[blockIdx.x], tab);
+  if (threadIdx.x == 0) out[blockIdx.x] = a;
+}
+
+int32_t mimo_calc_alpha(const double* ibo_db, int64_t n, double* out) {
+  if (n < 0) return sfail(MIMO_EINVAL, "n < 0");
+  if (n == 0) return MIMO_OK;
+  if (n > (1 << 30)) return sfail(MIMO_EINVAL, "n too large");
+  std::vector<double> g2(n);
+  for (int64_t i = 0; i < n; ++i) g2[i] = std::pow(10.0, ibo_db[i] / 10.0);  // gamma^2, modulation.py:186
+  const std::vector<double> tab = mimo::alpha_segment_table();
+  DBuf dg, dt, dout;
+  S_TRY(dg.alloc(n * sizeof(double)));
+  S_TRY(dt.alloc(tab.size() * sizeof(double)));
+  S_TRY(dout.alloc(n * sizeof(double)));
+  S_TRY(hipMemcpy(dg.p, g2.data(), n * sizeof(double), hipMemcpyHostToDevice));
+  S_TRY(hipMemcpy(dt.p, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_calc_alpha, dim3((unsigned)n), dim3(64), 0, 0, dg.as<double>(), dt.as<double>(), dout.as<double>());
+  S_TRY(hipGetLastError());
+  S_TRY(hipMemcpy(out, dout.p, n * sizeof(double), hipMemcpyDeviceToHost));
   return MIMO_OK;
 }
 

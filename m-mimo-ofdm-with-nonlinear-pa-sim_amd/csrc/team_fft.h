@@ -309,7 +309,9 @@ struct TeamFft {
   // exchange 0 drop 3x (tools/lds_conflicts.py; the model reproduces SQ_LDS_BANK_CONFLICT
   // of the 1/16 layout exactly, profiles/r02/pmc_f64_r1).  F = 8192 keeps 1/16: its 16 KiB
   // more would not fit the 160 KiB LDS next to the fp64 tables and the CSI scratch.
-  static constexpr int PADN = 5;  // one pad slot per 32 elements for exchanges >= 1
+  // Exchanges >= 1: one pad slot per 32 elements; fp64 from F 4096 one per 128 (modelled
+  // conflict-free as well, tests/test_lds_layout.py: 3 KiB of LDS back at F 8192).
+  static constexpr int PADN = (sizeof(Re) == 8 && F >= 4096) ? 7 : 5;
   // (fp64 F 4096 on 256 threads: 1/32, so that two teams fit a CU -- 80,256 B each)
   static constexpr int PAD0 = (sizeof(Re) == 8 && F < 8192) ? (F == 4096 && T == 256 ? 5 : 3) : 4;
   static constexpr int psh(int S) { return S == 0 ? PAD0 : PADN; }

@@ -30,6 +30,7 @@
 
 #include <type_traits>
 
+#include "alpha_fit.h"
 #include "philox.h"
 #include "team_fft.h"
 #include "wave_fft.h"
@@ -50,6 +51,7 @@ template <typename R>
 struct TrialParams {
   using C = cx<R>;
   uint64_t seed;
+  uint64_t csi_seed;             // CH_TABLE + CSI: key of the one shared estimate (mimo_config.csi_seed)
   uint64_t first_trial;
   uint32_t* counts;              // [n_trials][n_idx]
   const C* tw;                   // team-FFT stage twiddles of (F, T) (team_fft.h fft_tw_off)
@@ -264,14 +266,12 @@ __device__ __forceinline__ C pa_apply(int kind, C x, R sat, R sqrt_sat, R inv_sa
   return mkc(x.x * sc, x.y * sc);
 }
 
-// Cold paths out of line: the antenna loop's exact-alpha fallback (|x| > alpha_xlim) and
-// the general-hardness Rapp gain (library exp / erfc / log2 / exp2).  Inlined, their f64
-// constants were hoisted into the loop preheader and spilled to scratch once per trial
-// (~90 KB of writes per trial at config 2, profiles/r03/pmc); out of line they stay in
-// the call.  Measured: config 2 -2.5 %, CSI -2.7 %, LoS -2.3 %, two-path -3.0 %, F 8192
-// -0.4 %; F 4096 +1.6 %, so the 16-point F 4096 instance keeps them inline
-// (profiles/r03/ab_s/), as do the fp32 instances (not measured).
-__device__ __attribute__((noinline)) double alpha_of_gamma2_cold(double g2) { return alpha_of_gamma2(g2); }
+// Cold path out of line: the general-hardness Rapp gain (library log2 / exp2).  Inlined,
+// its f64 constants were hoisted into the loop preheader and spilled to scratch once per
+// trial (~90 KB of writes per trial at config 2, profiles/r03/pmc); out of line they stay
+// in the call.  Measured with the exact-alpha fallback (now alpha_fit.h's segment table,
+// which has no constants to hoist) outlined as well: config 2 -2.5 %, CSI -2.7 %, LoS
+// -2.3 %, two-path -3.0 %, F 8192 -0.4 %; F 4096 +1.6 % (profiles/r03/ab_s/).
 template <class C, typename R = real_of<C>>
 __device__ __attribute__((noinline)) C pa_rapp_general(C x, R inv_sat, R rapp_p) {
   return pa_apply(PA_RAPP, x, R(0), R(0), inv_sat, rapp_p, R(0));
@@ -604,10 +604,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   using CParams = const __attribute__((address_space(4))) TrialParams<R>;
   CParams& p = *(CParams*)(p0.points + pi);
   constexpr bool WAVEFFT = wave_fft_used(F, T, sizeof(R) == 8);
-  // CSI instances keep the stage-1 twiddles in global memory: their 4 KiB per-antenna power
-  // table plus the 1 KiB LDS copy would cross the 3-teams-per-CU line (LDS is allocated in
-  // 512-B granules: 54,368 B -> 54,784 B x 3 > 160 KiB; measured +10 % at 2 teams per CU).
-  using FFT = std::conditional_t<WAVEFFT, WaveFft<F, T, R, !CSI>, TeamFft<F, T, NBUF, R>>;
+  // CSI instances read only stage 1's twiddle block from LDS, not stage 2's rows: with
+  // their 4 KiB per-antenna power table the 3 KiB of rows would cross the 3-teams-per-CU
+  // line (LDS is allocated in 512-B granules; 2 teams per CU measured +10 %).  Before the
+  // transposed exchange 0 freed 2 KiB of the wave rows the stage-1 block did not fit
+  // either; with it: -0.7 % (profiles/r04/csi/).
+  using FFT = std::conditional_t<WAVEFFT, WaveFft<F, T, R, true, !CSI>, TeamFft<F, T, NBUF, R>>;
   using SL = Slots<F, T, NSLOT, ALIGNED>;
   using CHN = Channel<R, F, T, NSLOT, ALIGNED, CH>;
   constexpr int P = FFT::P;
@@ -624,9 +626,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   __shared__ R vk_part[2][T / 64];
   __shared__ R pw_csi[CSI ? kMaxCsiAnt : 1];  // per-antenna mean |H|^2 (CSI model)
   __shared__ C symw_s[SYMW_LDS ? NSLOT * T : 1];  // [slot][thread]
-  // wave-split FFT: the one-wave sub-transforms read stage 1's twiddles and stage 2's rows
-  // r = 3, 5, 6 from LDS (team_fft.h TWL_N; -24 f64 ops per antenna at config 2)
-  constexpr bool LTW1 = WAVEFFT && !CSI;
+  // wave-split FFT: the one-wave sub-transforms read stage 1's twiddles and (without CSI)
+  // stage 2's rows r = 3, 5, 6 from LDS (team_fft.h TWL_N; -24 f64 ops per antenna at config 2)
+  constexpr bool LTW1 = WAVEFFT;
   constexpr int TW1_N = [] {
     if constexpr (LTW1) return FFT::TWL_N; else return 1;
   }();
@@ -643,6 +645,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // reference draws the erroneous estimate once (Link.__init__, mp_model.py:87) and keeps
   // it for every trial, so all trials share one draw (trial-independent counter).
   const uint32_t csi_trial = CH == CH_TABLE ? kFixedCsiTrial : trial;
+  // ... and it belongs to the Link, not to the run: keyed by the engine's csi_seed
+  const Key csi_key = CH == CH_TABLE ? Key{(uint32_t)p.csi_seed, (uint32_t)(p.csi_seed >> 32)} : key;
   // Channel counter: the trial, or (diagnostic, chan_period > 0) the trial modulo the
   // period -- every group of chan_period trials replays one sequence of Rayleigh channels,
   // as the reference's forked workers all replay the channel object's seeded generator
@@ -715,13 +719,17 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     CHN::template gen<FREL>(p, key, ch_trial, a, tl, rx, h);
     if constexpr (CSI) {
       // mp_model.py:264-282: Hhat = sqrt(1-eps^2) H + eps sqrt(mean_k |H|^2) z
+      // (a team_sum -- two barriers -- per antenna: collecting every antenna's wave partials
+      // without barriers and regenerating |H|^2 in a pass before this one measured +8 % at
+      // config 2 geometry with CSI, profiles/r04/csi/: the barriers cost less than the
+      // extra channel draws)
       R pw = R(0);
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) pw = fmar(h[s].x, h[s].x, fmar(h[s].y, h[s].y, pw));
       pw = team_sum<T>(pw, red) / (R)S;
       if (t0) pw_csi[a] = pw;
       C zc[NSLOT];
-      CHN::normals(key, csi_trial, ST_CSI, (uint32_t)a, tl, S, zc);
+      CHN::normals(csi_key, csi_trial, ST_CSI, (uint32_t)a, tl, S, zc);
       const R sc = p.csi_b * sqrt_ieee(pw);
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s)
@@ -767,15 +775,28 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // |Hhat w|^2 = vk / F): -1.1 % at F 2048 (wave-split instances); +5 % at F 4096, where
   // the 16-point team's register allocation suffers (profiles/r03/ab_o/ab_paper.json).
   constexpr bool PRE_EW = SYMW_RE && WAVEFFT;
-  constexpr bool COLD_OUT = sizeof(R) == 8 && F != 4096;  // cold paths out of line (alpha_of_gamma2_cold)
+  // General-p Rapp out of line, and the alpha fallback by the segment table (alpha_fit.h),
+  // except for the 16-point F 4096 team, where both measured slower: the outlined Rapp
+  // +1.6 % (r03 ab_s), the segment table +1.1 % (profiles/r04/alpha/; same executed-path
+  // instruction count, cause not found), so it keeps the library forms inline.
+  constexpr bool COLD_OUT = sizeof(R) == 8 && F != 4096;
   constexpr bool E2_RE = sizeof(R) == 8 && !SYMW_LDS;    // off: +2.8 % at F 8192 (ab_diet_prefetch.json)
   C symw_r[SYMW_LDS || SYMW_RE ? 1 : NSLOT];
-  uint32_t slab_r[SYMW_RE ? NSLOT : 1];
+  // F 8192 (one team per CU, 256 VGPRs): the lattice levels live in LDS ([slot][thread],
+  // thread-private: no barrier), not in 8 VGPRs that the allocator reloaded from scratch
+  // per antenna.  (Not with CSI: its power table leaves no room.)
+  constexpr bool SLAB_LDS = SYMW_RE && F >= 8192 && !CSI && NSLOT * T * 4 <= 16384;
+  uint32_t slab_r[SYMW_RE && !SLAB_LDS ? NSLOT : 1];
+  __shared__ uint32_t slab_s[SLAB_LDS ? NSLOT * T : 1];
+  auto slab = [&](int s) __attribute__((always_inline)) -> uint32_t {
+    if constexpr (SLAB_LDS) return slab_s[s * T + t]; else return slab_r[s];
+  };
   auto set_symbols = [&](const uint32_t (&lab_in)[NSLOT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
       if constexpr (SYMW_RE) {
-        slab_r[s] = qam_levels(lab_in[s], L, hb);
+        if constexpr (SLAB_LDS) slab_s[s * T + t] = qam_levels(lab_in[s], L, hb);
+        else slab_r[s] = qam_levels(lab_in[s], L, hb);
       } else {
         const C v = cscale(qam_point<R>(lab_in[s], L, hb), inv_nrm[s] * inv_sqrt_f);
         if constexpr (SYMW_LDS) symw_s[s * T + t] = v; else symw_r[s] = v;
@@ -784,7 +805,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   };
   auto symw = [&](int s) __attribute__((always_inline)) -> C {
     if constexpr (SYMW_RE) {
-      uint32_t l = slab_r[s];
+      uint32_t l = slab(s);
       R in = inv_nrm[s];
       asm volatile("" : "+v"(l), "+v"(in));
       return cscale(levels_point<R>(l), in * inv_sqrt_f);
@@ -844,7 +865,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       C he[CSI ? NSLOT : 1];
       if constexpr (CSI) {
         C zc[NSLOT];
-        CHN::normals(key, csi_trial, ST_CSI, (uint32_t)a, tl, S, zc);
+        CHN::normals(csi_key, csi_trial, ST_CSI, (uint32_t)a, tl, S, zc);
         const R sc = p.csi_b * sqrt_ieee(pw_csi[a]);
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s)
@@ -863,7 +884,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
           // the lattice point times conj(Hhat w), w = 1 / ||Hhat|| / sqrt(F): vk accumulates
           // |Hhat w|^2 = |Hhat|^2 / ||Hhat||^2 / F directly (11 f64 ops per slot, not 13;
           // vk_scale restores the factor F)
-          uint32_t l = slab_r[s];
+          uint32_t l = slab(s);
           R in = inv_nrm[s];
           asm volatile("" : "+v"(l), "+v"(in));
           const C ew = cscale(e, in * inv_sqrt_f);
@@ -921,7 +942,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         } else {
           // (the register-diet pass sums vk / F: vks F is the precoding power)
           const R g2 = p.alpha_c / (PRE_EW ? vks * (R)F : vks);
-          if constexpr (COLD_OUT) alpha_a = alpha_of_gamma2_cold(g2); else alpha_a = alpha_of_gamma2(g2);
+          // fp64: the segment table (alpha_fit.h, appended to the Box-Muller tables in HBM)
+          if constexpr (COLD_OUT) alpha_a = alpha_seg(g2, reinterpret_cast<const double*>(p.lut + kLut64));
+          else alpha_a = alpha_of_gamma2(g2);
         }
       }
 #pragma unroll

@@ -51,7 +51,7 @@ constexpr int wave_fft_fw(int F, int T) { return F / (T / 64); }
 constexpr int wave_fft_tw_inter(int F, int T) { return fft_tw_total(wave_fft_fw(F, T), F / T); }
 constexpr int wave_fft_tw_total(int F, int T) { return wave_fft_tw_inter(F, T) + F; }
 
-template <int F, int T, typename Re, bool LTW1 = true>
+template <int F, int T, typename Re, bool LTW1 = true, bool LTW2 = LTW1>
 struct WaveFft {
   using C = cx<Re>;
   static constexpr int P = F / T;
@@ -62,7 +62,7 @@ struct WaveFft {
   // LTW1: stage-1 twiddles from LDS (tw1); from four waves on (F 2048) also stage 2's rows
   // r = 3, 5, 6 (config 2 -0.5 %, LoS -0.8 %, MCNC -1.0 %, profiles/r03/ab_x; at F 1024 the
   // 3 KiB more would cost the third wave per SIMD)
-  using Sub = TeamFft<FW, 64, 1, Re, true, LTW1, LTW1 && (T / 64) >= 4>;
+  using Sub = TeamFft<FW, 64, 1, Re, true, LTW1, LTW2 && (T / 64) >= 4>;
   static constexpr int TW1_N = Sub::TW1_N;
   static constexpr int TWL_N = Sub::TWL_N;         // tw1: LDS copy of the entries Sub::twl_src names
   static __device__ __forceinline__ int twl_src(int i) { return Sub::twl_src(i); }

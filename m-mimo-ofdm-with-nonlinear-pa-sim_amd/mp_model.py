@@ -137,14 +137,44 @@ def acquire_device_slot(dev: int) -> bool:
     return False
 
 
+def slot_heartbeat(dev: int) -> None:
+    """A slot holder's sign of life: touch its lock file (once before its engine set-up and
+    once per batch), so that waiting workers see progress even while the holder's first
+    batch -- engine creation, a 65,536-trial launch of a large array -- has not yet moved
+    the shared counters."""
+    fd = _SLOTS.get((os.getpid(), int(dev)))
+    if fd is not None:
+        try:
+            os.utime(fd)
+        except OSError:
+            pass
+
+
+def slot_activity(dev: int) -> int:
+    """Latest heartbeat (lock-file mtime, ns) of ``dev``'s slots; 0 if none."""
+    d = _slot_dir()
+    cap = max(1, int(os.environ.get("MIMO_MAX_ENGINES_PER_DEVICE", "2")))
+    latest = 0
+    for k in range(cap):
+        try:
+            latest = max(latest, os.stat(os.path.join(d, "dev%d_slot%d.lock" % (dev, k))).st_mtime_ns)
+        except OSError:
+            pass
+    return latest
+
+
 def wait_for_device_slot(dev: int, still_open, progress, stall_s: float = None, poll_s: float = 0.02) -> bool:
     """Wait for an engine slot on ``dev`` while the shared counters are open.  Returns False
     when the counters closed (the slot holders finished the point: nothing left to do), True
-    once a slot is held -- or when the counters made no progress for ``stall_s`` seconds
-    (MIMO_SLOT_STALL_S, default 30): the slots are then held by processes that do not work
-    on these counters, and this worker creates its engine beyond MIMO_MAX_ENGINES_PER_DEVICE
-    rather than wait forever."""
+    once a slot is held -- or when neither the counters nor the slot holders' heartbeats
+    (slot_heartbeat) moved for ``stall_s`` seconds (MIMO_SLOT_STALL_S, default 30): the slots
+    are then held by processes that do not work, and this worker creates its engine beyond
+    MIMO_MAX_ENGINES_PER_DEVICE rather than wait forever."""
     stall_s = float(os.environ.get("MIMO_SLOT_STALL_S", "30")) if stall_s is None else stall_s
+    base = progress
+
+    def progress():
+        return (base(), slot_activity(dev))
     last, t_last = progress(), time.monotonic()
     while not acquire_device_slot(dev):
         if not still_open():
@@ -191,6 +221,10 @@ class Link:
         self.loc_rng = np.random.default_rng(1)
         self.bit_rng = np.random.default_rng(2)
         self.my_csi_noise.rng_gen = np.random.default_rng(3)
+        # the fixed-channel (reroll_chan=False) CSI estimate is the Link's, drawn once from its
+        # own CSI generator (seed 3 above, mp_model.py:76-87): its Philox key, shared by every
+        # worker and every simulate() call whatever their seed_arr
+        self.csi_seed = _seed64([3, 0xC51])
         self.rx_loc_var = rx_loc_var
         self.n_ant_val = len(self.my_array.array_elements)
         self.n_bits_per_ofdm_sym = self.my_mod.n_bits_per_ofdm_sym
@@ -235,7 +269,7 @@ class Link:
                 "mcnc" if self.is_mcnc else "cnc", self.my_array.positions(),
                 (self.rx_loc_x, self.rx_loc_y, rx.cord_z), self.rx_loc_var,
                 channel.carrier_freqs(m.n_fft, rx.carrier_spacing, rx.center_freq), reroll=reroll_chan, device=dev,
-                precision=self.precision, chan_table=table)
+                precision=self.precision, chan_table=table, csi_seed=self.csi_seed if table is not None else 0)
             self._engine_key = key
         self._push_point()
         return self._engine
@@ -285,6 +319,7 @@ class Link:
                 return
         else:
             acquire_device_slot(dev)  # private counters: nobody else closes them, never wait
+        slot_heartbeat(dev)
         eng = self.engine(reroll_chan)
         seed = _seed64(seed_arr)
         iters_all = np.asarray(cnc_n_iter_lst, dtype=np.int64).reshape(-1)
@@ -307,6 +342,7 @@ class Link:
                            self.max_batch)
             uniq = sorted(set(run_iters))
             e, b, _ = eng.run(seed, trial, n, uniq, clean_on)
+            slot_heartbeat(dev)
             trial += n
             pos = {it: j + (1 if clean_on else 0) for j, it in enumerate(uniq)}
             lock = n_err_shared_arr.get_lock() if hasattr(n_err_shared_arr, "get_lock") else None

@@ -28,6 +28,45 @@ import numpy as np
 from utilities import ebn0_to_snr, save_to_csv
 
 
+# BASELINE config 4 at its stated extent (SNR 0-30 dB x IBO 0-7 dB): Eb/N0
+# 0..30 dB x IBO 0..7 dB in 0.5 dB steps = 915 points, receiver iterations 0..8, the fixed-BER
+# driver's stopping rule and geometry (main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:40-61,
+# 100-215: 64-antenna ULA, FFT 4096, 2048 sub-carriers, 64-QAM, soft limiter).
+BASELINE_C4 = dict(ibo=np.arange(0.0, 7.01, 0.5), ebn0=np.arange(0.0, 30.01, 0.5), iters=np.arange(0, 9),
+                   n_ant=64, n_sc=2048, n_fft=4096, qam=64, cp=128, bits_sent_max=int(5e6), n_err_min=int(1e5))
+
+
+def paper_link(channel="rayleigh", receiver="cnc", precision="f64", device=None, n_ant=64, n_sc=2048, n_fft=4096,
+               qam=64, cp=128, n_err_min=int(1e5), bits_sent_max=int(5e6)):
+    """The reference drivers' Link (main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:40-98):
+    ULA at z = 15 m, RX at (212, 212, 1.5), 3.5 GHz / 15 kHz, soft limiter, seed-1234 Rayleigh."""
+    import copy
+
+    import antenna_array
+    import channel as ch_mod
+    import distortion
+    import modulation
+    import mp_model
+    import noise
+    import transceiver
+    mod = modulation.OfdmQamModem(constel_size=qam, n_fft=n_fft, n_sub_carr=n_sc, cp_len=cp)
+    dist_obj = distortion.SoftLimiter(0, mod.avg_sample_power)
+    tx = transceiver.Transceiver(modem=copy.deepcopy(mod), impairment=copy.deepcopy(dist_obj), center_freq=int(3.5e9),
+                                 carrier_spacing=int(15e3))
+    rx = transceiver.Transceiver(modem=copy.deepcopy(mod), impairment=copy.deepcopy(dist_obj), cord_x=212,
+                                 cord_y=212, cord_z=1.5, center_freq=int(3.5e9), carrier_spacing=int(15e3))
+    arr = antenna_array.LinearArray(n_elements=n_ant, base_transceiver=tx, center_freq=int(3.5e9),
+                                    wav_len_spacing=0.5, cord_x=0, cord_y=0, cord_z=15)
+    if channel == "rayleigh":
+        ch = ch_mod.MisoRayleighFd(tx_transceivers=arr.array_elements, rx_transceiver=rx, seed=1234)
+    else:
+        ch = ch_mod.MisoLosFd() if channel == "los" else ch_mod.MisoTwoPathFd()
+        ch.calc_channel_mat(tx_transceivers=arr.array_elements, rx_transceiver=rx, skip_attenuation=False)
+    return mp_model.Link(mod_obj=mod, array_obj=arr, std_rx_obj=rx, chan_obj=ch, noise_obj=noise.Awgn(snr_db=10),
+                         rx_loc_var=10.0, n_err_min=n_err_min, bits_sent_max=bits_sent_max,
+                         is_mcnc=receiver == "mcnc", device=device, precision=precision)
+
+
 def point_seed(base_seed: int, point_index: int) -> list:
     """Seed array of one grid point (fed to Link.simulate, which hashes it)."""
     return [int(base_seed) & 0x7FFFFFFFFFFFFFFF, int(point_index), 0x5EED]

@@ -48,6 +48,7 @@ class SimConfig:
     reroll: bool = True
     tx_pos: np.ndarray | None = field(default=None, repr=False)
     table_h: np.ndarray | None = field(default=None, repr=False)  # [A, F] channel_mat_fd for "table"
+    csi_seed: int | None = None    # "table" + CSI: key of the one shared estimate (None: the run seed)
 
     def __post_init__(self):
         if self.tx_pos is None:
@@ -186,8 +187,11 @@ def draws(cfg: SimConfig, seed: int, trials):
         # a fixed channel (reroll_chan=False) keeps the one erroneous estimate Link.__init__
         # drew (mp_model.py:87; set_precoding_and_recalculate_agc is not called in the loop,
         # :190-206): every trial reads the same, trial-independent CSI draw
-        csi_trials = np.full_like(trials, FIXED_CSI_TRIAL) if cfg.channel == "table" else trials
-        out["z_csi"] = philox.csi_normals(seed, csi_trials, cfg.n_sc, cfg.n_ant)
+        # and, as the estimate belongs to the Link, from the Link's own key (csi_seed), not the run's
+        fixed = cfg.channel == "table"
+        csi_trials = np.full_like(trials, FIXED_CSI_TRIAL) if fixed else trials
+        csi_key = cfg.csi_seed if fixed and cfg.csi_seed else seed
+        out["z_csi"] = philox.csi_normals(csi_key, csi_trials, cfg.n_sc, cfg.n_ant)
     return out
 
 

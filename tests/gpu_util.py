@@ -13,7 +13,8 @@ def engine_for(cfg: SimConfig, device=-1, precision=None):
     carriers = rm.fftfreq_carriers(cfg.n_fft, cfg.carrier_spacing, cfg.center_freq)
     eng = _engine.Engine(cfg.n_ant, cfg.n_sc, cfg.n_fft, cfg.constel_size, 4, cfg.channel, cfg.receiver, cfg.tx_pos,
                          cfg.rx_pos, cfg.rx_loc_var, carriers, reroll=cfg.reroll, device=device, precision=precision,
-                         chan_table=cfg.table_h if cfg.channel == "table" else None)
+                         chan_table=cfg.table_h if cfg.channel == "table" else None,
+                         csi_seed=cfg.csi_seed or 0)
     pp = point_params(cfg)
     avg = pp["avg_samp"] / cfg.n_ant  # MRT: mean |P|^2 = 1/A (antenna_array.py:328-335)
     if cfg.pa == "toi":

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     lib = _engine.lib()
     missing = [n for n in declared_functions() if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.mimo_abi_version() == 5
+    assert lib.mimo_abi_version() == 6
 
 
 def _cfg(**kw):

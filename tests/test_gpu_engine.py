@@ -10,6 +10,8 @@ a single sub-carrier of a single trial would fail them.  Statistically (batch me
 trials) the device BER must lie within 1 sigma-equivalent of the oracle's (tested with a
 3-sigma bound on the paired difference, far tighter than the unpaired 1-sigma criterion).
 """
+import dataclasses
+
 import numpy as np
 import pytest
 
@@ -123,6 +125,27 @@ def test_table_channel_vs_oracle(receiver, csi, prec):
     print("table", receiver, csi, eng.describe(), per.sum(0), ref.sum(0))
     assert "ch=4" in eng.describe()
     assert_counts_equal(per, ref, f"table {receiver} {csi} {prec}")
+
+
+@pytest.mark.parametrize("prec", PRECISIONS)
+def test_table_channel_csi_estimate_belongs_to_the_link(prec):
+    """with a fixed channel the erroneous estimate is the Link's (Link.__init__
+    draws it once, mp_model.py:76-87), not the run's: engines keyed by mimo_config.csi_seed
+    give runs with different seeds (the forked workers of one point) the same estimate --
+    each run equals the oracle with the SAME csi_seed and its own run seed, exactly."""
+    rng = np.random.default_rng(78)
+    A, S, F = 8, 256, 512
+    h = (rng.standard_normal((A, F)) + 1j * rng.standard_normal((A, F))) * np.sqrt(0.5) * 3e-7
+    cfg = sim.SimConfig(A, S, F, 16, ibo_db=1.0, snr_db=14.0, channel="table", receiver="cnc", csi_eps=0.3,
+                        table_h=h, csi_seed=0xC0FFEE1234)
+    eng = engine_for(cfg, precision=prec)
+    for seed in (19, 20):
+        ref = sim.run_trials(cfg, seed, np.arange(32), iters=[0, 1], incl_clean=True)
+        _, _, per = eng.run(seed, 0, 32, [0, 1], True, per_trial=True)
+        assert_counts_equal(per, ref, f"table csi seed {seed} {prec}")
+    # the run seed does not reach the estimate: the oracle keyed by the run seed differs
+    other = sim.run_trials(dataclasses.replace(cfg, csi_seed=None), 20, np.arange(32), iters=[0, 1], incl_clean=True)
+    assert not np.array_equal(other, per)
 
 
 def test_link_fixed_rayleigh_channel_equals_table_engine():

@@ -52,6 +52,27 @@ def test_pa_models(units):
     np.testing.assert_allclose(distortion.ThirdOrderNonLin(12, 20.95).process(x), units["pa_toi_out"], rtol=1e-12)
 
 
+def test_calc_alpha_vs_reference_and_mpmath(units):
+    """The float64 kernels' Bussgang gain outside the per-point fit (alpha_fit.h segment
+    table, mimo_calc_alpha): the reference's own calc_alpha outputs (units.npz, NumPy /
+    SciPy float64) within 4e-16 relative, and the 40-digit formula (mpmath) within 4e-16
+    relative (2 ulp) from g = 0.002 to g = 7 (IBO -54 ... +17 dB; alpha = 1 from g 6.5 on)."""
+    import _engine
+    np.testing.assert_allclose(_engine.calc_alpha(units["alpha_ibo"]), units["alpha_out"], rtol=4e-16, atol=0)
+    mpmath = pytest.importorskip("mpmath")
+    mpmath.mp.dps = 40
+    g = np.concatenate([np.geomspace(2e-3, 0.5, 300), np.linspace(0.5, 7.0, 1301)])
+    ibo = 20.0 * np.log10(g)
+    got = _engine.calc_alpha(ibo)
+    worst = 0.0
+    for g2, ai in zip(10.0 ** (ibo / 10.0), got):  # the float64 gamma^2 the host hands the kernel
+        gm = mpmath.sqrt(mpmath.mpf(float(g2)))
+        ref = 1 - mpmath.exp(-gm * gm) + mpmath.sqrt(mpmath.pi) / 2 * gm * mpmath.erfc(gm)
+        worst = max(worst, float(abs((mpmath.mpf(float(ai)) - ref) / ref)))
+    print("max relative error vs mpmath", worst)
+    assert worst <= 4e-16
+
+
 @pytest.mark.parametrize("F,S,cp", [(128, 64, 4), (2048, 1024, 128)])
 def test_ofdm_tx_rx(units, F, S, cp):
     import modulation

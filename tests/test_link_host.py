@@ -4,6 +4,8 @@ fake engine standing in for libmimo_engine."""
 import ctypes
 import multiprocessing as mp
 
+import os
+
 import numpy as np
 import pytest
 
@@ -231,6 +233,54 @@ def test_slot_wait_is_bounded_when_counters_stall(tmp_path, monkeypatch):
         state["n"] += 1
         return state["n"] < 5
     assert not mp_model.wait_for_device_slot(0, still_open, lambda: state["n"], stall_s=60)
+
+
+def _slow_holder(lock_dir, beat, hold_s, q):
+    """A slot holder whose counters do not move for hold_s (engine set-up, a long first
+    batch); with beat it touches its slot's heartbeat every 0.2 s."""
+    import os
+    import time
+    os.environ["MIMO_LOCK_DIR"] = lock_dir
+    os.environ["MIMO_MAX_ENGINES_PER_DEVICE"] = "1"
+    import mp_model
+    q.put(mp_model.acquire_device_slot(0))
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < hold_s:
+        if beat:
+            mp_model.slot_heartbeat(0)
+        time.sleep(0.2)
+
+
+@pytest.mark.parametrize("beat", [True, False])
+def test_slot_wait_counts_holder_heartbeats_as_progress(tmp_path, monkeypatch, beat):
+    """a holder whose first batch outlasts the stall time still counts as working
+    when it beats its slot's heartbeat: the waiter keeps waiting (no extra engine) and takes
+    the slot when the holder exits.  Without heartbeats the waiter gives up after stall_s."""
+    import time
+    import warnings
+    import mp_model
+    monkeypatch.setenv("MIMO_LOCK_DIR", str(tmp_path))
+    monkeypatch.setenv("MIMO_MAX_ENGINES_PER_DEVICE", "1")
+    monkeypatch.setattr(mp_model, "_SLOTS", {})  # this process holds no slot yet
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    hold = 3.0
+    p = ctx.Process(target=_slow_holder, args=(str(tmp_path), beat, hold, q))
+    p.start()
+    assert q.get(timeout=60) is True
+    t0 = time.monotonic()
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        got = mp_model.wait_for_device_slot(0, lambda: True, lambda: (0.0, 0.0), stall_s=1.0, poll_s=0.05)
+    waited = time.monotonic() - t0
+    p.join(60)
+    assert got is True
+    gave_up = any("MIMO_MAX_ENGINES_PER_DEVICE" in str(x.message) for x in w)
+    if beat:
+        assert not gave_up and waited >= hold - 0.5, (waited, [str(x.message) for x in w])
+        assert (os.getpid(), 0) in mp_model._SLOTS  # the freed slot is now this process's
+    else:
+        assert gave_up and waited < hold - 0.5, waited
 
 
 def test_simulate_points_rejects_counters_it_cannot_add_into(monkeypatch):

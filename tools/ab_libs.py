@@ -7,6 +7,7 @@ alternate between them round by round.  Prints median / min kernel ms per launch
 error totals (builds that differ only in fp32 rounding agree to a few errors in 1e7 bits).
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -33,7 +34,14 @@ def main():
     handles, engines = [], []
     for path in args.libs:
         _engine._lib, _engine.LIB_PATH = None, os.path.abspath(path)
+        # an older build may predate entry points the binding lists: bind what it exports
+        probe = ctypes.CDLL(_engine.LIB_PATH)
+        saved = dict(_engine.SYMBOLS)
+        for name in [n for n in saved if not hasattr(probe, n)]:
+            del _engine.SYMBOLS[name]
         handles.append(_engine.lib())
+        _engine.SYMBOLS.clear()
+        _engine.SYMBOLS.update(saved)
         engines.append(bench.make_engine(0, args.workload, args.precision))
     res = {i: [] for i in range(len(engines))}
     errs = {}

@@ -31,7 +31,6 @@ and the 400 points it shares with the published grid agree with it (z-scores).
 from __future__ import annotations
 
 import argparse
-import copy
 import json
 import os
 import sys
@@ -63,29 +62,9 @@ def published(channel, receiver):
 
 
 def build_link(channel, receiver, precision):
-    import antenna_array
-    import channel as ch_mod
-    import distortion
-    import modulation
-    import mp_model
-    import noise
-    import transceiver
-    mod = modulation.OfdmQamModem(constel_size=M, n_fft=N_FFT, n_sub_carr=N_SC, cp_len=CP)
-    dist = distortion.SoftLimiter(0, mod.avg_sample_power)
-    tx = transceiver.Transceiver(modem=copy.deepcopy(mod), impairment=copy.deepcopy(dist), center_freq=int(3.5e9),
-                                 carrier_spacing=int(15e3))
-    rx = transceiver.Transceiver(modem=copy.deepcopy(mod), impairment=copy.deepcopy(dist), cord_x=212, cord_y=212,
-                                 cord_z=1.5, center_freq=int(3.5e9), carrier_spacing=int(15e3))
-    arr = antenna_array.LinearArray(n_elements=N_ANT, base_transceiver=tx, center_freq=int(3.5e9),
-                                    wav_len_spacing=0.5, cord_x=0, cord_y=0, cord_z=15)
-    if channel == "rayleigh":
-        ch = ch_mod.MisoRayleighFd(tx_transceivers=arr.array_elements, rx_transceiver=rx, seed=1234)
-    else:
-        ch = ch_mod.MisoLosFd() if channel == "los" else ch_mod.MisoTwoPathFd()
-        ch.calc_channel_mat(tx_transceivers=arr.array_elements, rx_transceiver=rx, skip_attenuation=False)
-    return mp_model.Link(mod_obj=mod, array_obj=arr, std_rx_obj=rx, chan_obj=ch, noise_obj=noise.Awgn(snr_db=10),
-                         rx_loc_var=10.0, n_err_min=N_ERR_MIN, bits_sent_max=BITS_MAX, is_mcnc=receiver == "mcnc",
-                         precision=precision)
+    import sweep
+    return sweep.paper_link(channel, receiver, precision, n_ant=N_ANT, n_sc=N_SC, n_fft=N_FFT, qam=M, cp=CP,
+                            n_err_min=N_ERR_MIN, bits_sent_max=BITS_MAX)
 
 
 def reference_trials(pub_ber, bits_per_sym, per_counter=False):
@@ -147,6 +126,7 @@ def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137)
     fin = np.isfinite(req_gpu) & np.isfinite(req_pub)
     dreq = np.abs(req_gpu[fin] - req_pub[fin])  # only where both are finite (no inf - inf)
     n_sym = int(trials.sum())
+    spread = spread_stats(z, sel, pub)
     out = dict(channel=channel, receiver=receiver, precision=precision, points=int(P), ofdm_symbols=n_sym,
                wall_s=round(wall, 3), symbols_per_s=round(n_sym / wall, 1), compared=int(sel.sum()),
                max_abs_z=round(float(np.abs(z).max()), 3), p95_abs_z=round(float(np.percentile(np.abs(z[sel]), 95)), 3),
@@ -164,11 +144,86 @@ def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137)
                req_ebn0_at_ber_1e2=dict(finite_mismatch=int((np.isfinite(req_gpu) != np.isfinite(req_pub)).sum()),
                                      compared=int(fin.sum()),
                                      mean_abs_db=round(float(dreq.mean()), 4) if dreq.size else None,
-                                     max_abs_db=round(float(dreq.max()), 4) if dreq.size else None))
+                                     max_abs_db=round(float(dreq.max()), 4) if dreq.size else None),
+               spread=spread)
     return out, ber, pub, z
 
 
-BASE_IBO = np.arange(0.0, 7.01, 0.5)    # 15 points
+def spread_stats(z, sel, pub=None):
+    """Where the excess spread of z sits.  z: [ibo, ebn0, iteration],
+    sel: compared entries.
+
+    The 9 iteration counters of a point share its trials (ours and the reference's), so
+    their z are nearly one variable: ``within_point_corr`` (z of iterations i, i+1 at the
+    same point) is reported, and the row / lag statistics use the POINT z (mean over the
+    point's compared iterations).  Reported:
+    * per iteration column: mean z over points (a calibration or physics mismatch of one
+      receiver iteration shows here; bound 3 / sqrt(n) for n independent points);
+    * per IBO row: mean point z, bounded by 3 sqrt(v / n) with v the measured variance of
+      the point z (a signed mismatch confined to an IBO region shows here);
+    * lag-1 autocorrelation of the point z along Eb/N0 within each IBO row: estimates whose
+      points share randomness (the reference replaying one seeded channel sequence at
+      every point, channel.py:209-212, mp_model.py:61) give positive values, independent
+      per-point errors ~0 (bound 3 / sqrt(pairs));
+    * the point-z variance (1 if the sigma model holds), split by stopping-rule regime
+      (budget-limited: every counter below BER 2e-2 closes at bits_sent_max) and by IBO."""
+    n_ibo, n_ebn0, n_it = z.shape
+    pz = np.full((n_ibo, n_ebn0), np.nan)
+    for i in range(n_ibo):
+        for j in range(n_ebn0):
+            if sel[i, j].sum() >= 1:
+                pz[i, j] = z[i, j][sel[i, j]].mean()
+    ok = np.isfinite(pz)
+    v = float(np.nanvar(pz))
+    a, b = [], []
+    for i in range(n_ibo):
+        for it in range(n_it - 1):
+            m = sel[i, :, it] & sel[i, :, it + 1]
+            a += list(z[i, m, it])
+            b += list(z[i, m, it + 1])
+    wcorr = float(np.corrcoef(a, b)[0, 1]) if len(a) > 2 else float("nan")
+    cols = []
+    for it in range(n_it):
+        zz = z[..., it][sel[..., it]]
+        if zz.size:
+            m = float(zz.mean())
+            cols.append(dict(iteration=it, n=int(zz.size), mean_z=round(m, 3), mean_z2=round(float((zz ** 2).mean()), 3),
+                             bound=round(3 / np.sqrt(zz.size), 3), outside=bool(abs(m) > 3 / np.sqrt(zz.size))))
+    rows = []
+    for i in range(n_ibo):
+        zz = pz[i][ok[i]]
+        if zz.size:
+            m, bd = float(zz.mean()), 3 * np.sqrt(v / zz.size)
+            rows.append(dict(ibo_index=i, n_points=int(zz.size), mean_point_z=round(m, 3), bound=round(float(bd), 3),
+                             outside=bool(abs(m) > bd)))
+    num = d0 = d1 = 0.0
+    pairs = 0
+    for i in range(n_ibo):
+        m = ok[i, 1:] & ok[i, :-1]
+        x, y = pz[i, :-1][m], pz[i, 1:][m]
+        num += float((x * y).sum())
+        d0 += float((x * x).sum())
+        d1 += float((y * y).sum())
+        pairs += int(m.sum())
+    lag1 = num / np.sqrt(d0 * d1) if d0 > 0 and d1 > 0 else float("nan")
+    out = dict(within_point_corr=round(wcorr, 3), n_points=int(ok.sum()), point_z_var=round(v, 3),
+               iterations=cols, rows=rows, lag1_point_z_along_ebn0=round(float(lag1), 4), lag1_pairs=pairs,
+               lag1_bound=round(3 / np.sqrt(max(pairs, 1)), 4),
+               iterations_outside=sum(c["outside"] for c in cols), rows_outside=sum(r["outside"] for r in rows))
+    if pub is not None:
+        budget = np.array([[sel[i, j].any() and pub[i, j][sel[i, j]].max() < 2e-2 for j in range(n_ebn0)]
+                           for i in range(n_ibo)]) & ok
+        half = np.zeros_like(ok)
+        half[: n_ibo // 2 - 2] = True
+        out["point_z_var_by_regime"] = dict(
+            budget_limited=dict(n=int(budget.sum()), var=round(float(np.var(pz[budget])), 3) if budget.any() else None),
+            error_limited=dict(n=int((ok & ~budget).sum()), var=round(float(np.var(pz[ok & ~budget])), 3)),
+            ibo_below_3db=dict(n=int((ok & half).sum()), var=round(float(np.var(pz[ok & half])), 3)),
+            ibo_from_3db=dict(n=int((ok & ~half).sum()), var=round(float(np.var(pz[ok & ~half])), 3)))
+    return out
+
+
+BASE_IBO = np.arange(0.0, 7.01, 0.5)    # 15 points (sweep.BASELINE_C4)
 BASE_EBN0 = np.arange(0.0, 30.01, 0.5)  # 61 points
 
 

@@ -95,9 +95,12 @@ def xpose_layout(F, T, dw):
     return lambda e: (e % R0) * xs + e // R0
 
 
-def production_costs(F, T, dw, padn=5):
+def production_costs(F, T, dw, padn=None):
     """Extra cycles per transform of every exchange in the production layout (XP0 for
-    exchange 0 when R0 >= 4, 1/2^padn linear padding after)."""
+    exchange 0 when R0 >= 4, 1/2^padn linear padding after: team_fft.h PADN, 1/128 for fp64
+    from F 4096, 1/32 otherwise)."""
+    if padn is None:
+        padn = 7 if dw == 4 and F >= 4096 else 5
     P, st = stages(F, T)
     out = []
     for s in range(len(st) - 1):
