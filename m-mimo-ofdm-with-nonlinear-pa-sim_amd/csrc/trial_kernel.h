@@ -51,7 +51,6 @@ template <typename R>
 struct TrialParams {
   using C = cx<R>;
   uint64_t seed;
-  uint64_t csi_seed;             // CH_TABLE + CSI: key of the one shared estimate (mimo_config.csi_seed)
   uint64_t first_trial;
   uint32_t* counts;              // [n_trials][n_idx]
   const C* tw;                   // team-FFT stage twiddles of (F, T) (team_fft.h fft_tw_off)
@@ -96,6 +95,10 @@ struct TrialParams {
   const uint32_t* point_start;   // [n_points + 1] block offsets (device)
   int n_points;
   uint32_t chan_period;          // 0, or the channel-replay period (mimo_config.chan_replay_period)
+  // Last, so that the fields the antenna loop reloads keep their 16-byte alignment (the
+  // scalar loads pair them as s_load_dwordx4; inserted after `seed` it cost the F 4096
+  // instance 1 %, profiles/r04/misc/).
+  uint64_t csi_seed;             // CH_TABLE + CSI: key of the one shared estimate (mimo_config.csi_seed)
 };
 
 // Ablation switches for cost breakdowns.  Compiled in only with -DMIMO_ABLATION
@@ -690,12 +693,15 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     valid_mask |= (v ? 1u : 0u) << s;
   }
 
+  // (the thread id laundered per use: the table reads before and after the antenna loop
+  // are redone, not kept live across it -- 8 doubles per thread that the F 8192 instance
+  // spilled once per trial)
   auto frel_of = [&](int s) __attribute__((always_inline)) -> R {
     if constexpr (FREL) {
       return R(1);
     } else {
       bool v;
-      const int k = SL::k_of(s, t, S, v);
+      const int k = SL::k_of(s, opaque(t), S, v);
       return v ? p.f_rel[k] : R(1);
     }
   };
@@ -777,8 +783,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   constexpr bool PRE_EW = SYMW_RE && WAVEFFT;
   // General-p Rapp out of line, and the alpha fallback by the segment table (alpha_fit.h),
   // except for the 16-point F 4096 team, where both measured slower: the outlined Rapp
-  // +1.6 % (r03 ab_s), the segment table +1.1 % (profiles/r04/alpha/; same executed-path
-  // instruction count, cause not found), so it keeps the library forms inline.
+  // +1.6 % (r03 ab_s); both with the segment table +0.8 % (profiles/r04/alpha/), so it
+  // keeps the library forms inline.
   constexpr bool COLD_OUT = sizeof(R) == 8 && F != 4096;
   constexpr bool E2_RE = sizeof(R) == 8 && !SYMW_LDS;    // off: +2.8 % at F 8192 (ab_diet_prefetch.json)
   C symw_r[SYMW_LDS || SYMW_RE ? 1 : NSLOT];
