@@ -18,7 +18,7 @@ set -o pipefail
 export TMPDIR=/tmp
 MODE=$1; O=$2; shift 2
 mkdir -p "$O"
-N="--no-cpu-baseline"
+N="--no-cpu-baseline --no-grid"  # bench lines and counter passes: the headline kernel only
 
 line() {  # line <name> <bench args...>
   local name=$1; shift
