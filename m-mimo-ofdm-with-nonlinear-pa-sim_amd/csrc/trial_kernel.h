@@ -377,6 +377,18 @@ __device__ __forceinline__ uint32_t qam_levels(uint32_t label, int L, int hb) {
   const int ii = 2 * (int)gray_inv(label >> hb) - (L - 1), iq = 2 * (int)gray_inv(label & ((1u << hb) - 1u)) - (L - 1);
   return ((uint32_t)ii << 16) | ((uint32_t)iq & 0xFFFFu);
 }
+// Two slots per word for the register diet: int8 lattice levels (|level| <= L - 1 <= 63 for
+// M <= 4096), slot 2 i + h in bits 16 h .. 16 h + 15 of word i (I high byte): half the VGPRs
+// of one word per slot, and the same 2 extracts + 2 converts (v_bfe_i32) to rebuild.
+__device__ __forceinline__ uint32_t qam_levels8(uint32_t label, int L, int hb) {
+  const int ii = 2 * (int)gray_inv(label >> hb) - (L - 1), iq = 2 * (int)gray_inv(label & ((1u << hb) - 1u)) - (L - 1);
+  return (((uint32_t)ii & 0xFFu) << 8) | ((uint32_t)iq & 0xFFu);
+}
+template <typename R, int H>
+__device__ __forceinline__ cx<R> levels_point8(uint32_t w) {
+  // sign-extending extracts of bits 16 H + 8 .. + 15 (I) and 16 H .. + 7 (Q)
+  return mkc((R)((int)(w << (16 - 16 * H)) >> 24), (R)((int)(w << (24 - 16 * H)) >> 24));
+}
 template <typename R>
 __device__ __forceinline__ cx<R> levels_point(uint32_t v) {
   return mkc((R)((int)v >> 16), (R)(int)(int16_t)(v & 0xFFFFu));
@@ -792,17 +804,40 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // thread-private: no barrier), not in 8 VGPRs that the allocator reloaded from scratch
   // per antenna.  (Not with CSI: its power table leaves no room.)
   constexpr bool SLAB_LDS = SYMW_RE && F >= 8192 && !CSI && NSLOT * T * 4 <= 16384;
-  uint32_t slab_r[SYMW_RE && !SLAB_LDS ? NSLOT : 1];
+  // In registers at F 4096 (256 VGPRs, 12 scratch reloads per antenna): two slots per word
+  // (qam_levels8), -2.2 % on the paper config; at F 2048 (168 VGPRs, no reloads in the loop)
+  // one word per slot, the packed form measured neutral to +0.3 % (profiles/r04/levels8/).
+  constexpr bool SLAB8 = SYMW_RE && !SLAB_LDS && F == 4096;
+  uint32_t slab_r[SYMW_RE && !SLAB_LDS ? (SLAB8 ? NSLOT / 2 : NSLOT) : 1];
   __shared__ uint32_t slab_s[SLAB_LDS ? NSLOT * T : 1];
-  auto slab = [&](int s) __attribute__((always_inline)) -> uint32_t {
-    if constexpr (SLAB_LDS) return slab_s[s * T + t]; else return slab_r[s];
+  // the lattice point of slot s (the word laundered: rebuilt per antenna, not hoisted)
+  auto slab_point = [&](int s) __attribute__((always_inline)) -> C {
+    if constexpr (SLAB_LDS) {
+      uint32_t l = slab_s[s * T + t];
+      asm volatile("" : "+v"(l));
+      return levels_point<R>(l);
+    } else if constexpr (SLAB8) {
+      uint32_t w = slab_r[s >> 1];
+      asm volatile("" : "+v"(w));
+      return (s & 1) ? levels_point8<R, 1>(w) : levels_point8<R, 0>(w);
+    } else {
+      uint32_t l = slab_r[s];
+      asm volatile("" : "+v"(l));
+      return levels_point<R>(l);
+    }
   };
   auto set_symbols = [&](const uint32_t (&lab_in)[NSLOT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
       if constexpr (SYMW_RE) {
-        if constexpr (SLAB_LDS) slab_s[s * T + t] = qam_levels(lab_in[s], L, hb);
-        else slab_r[s] = qam_levels(lab_in[s], L, hb);
+        if constexpr (SLAB_LDS) {
+          slab_s[s * T + t] = qam_levels(lab_in[s], L, hb);
+        } else if constexpr (SLAB8) {
+          const uint32_t v = qam_levels8(lab_in[s], L, hb);
+          slab_r[s >> 1] = (s & 1) ? (slab_r[s >> 1] | (v << 16)) : v;
+        } else {
+          slab_r[s] = qam_levels(lab_in[s], L, hb);
+        }
       } else {
         const C v = cscale(qam_point<R>(lab_in[s], L, hb), inv_nrm[s] * inv_sqrt_f);
         if constexpr (SYMW_LDS) symw_s[s * T + t] = v; else symw_r[s] = v;
@@ -811,10 +846,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   };
   auto symw = [&](int s) __attribute__((always_inline)) -> C {
     if constexpr (SYMW_RE) {
-      uint32_t l = slab(s);
       R in = inv_nrm[s];
-      asm volatile("" : "+v"(l), "+v"(in));
-      return cscale(levels_point<R>(l), in * inv_sqrt_f);
+      asm volatile("" : "+v"(in));
+      return cscale(slab_point(s), in * inv_sqrt_f);
     } else if constexpr (SYMW_LDS) {
       return symw_s[s * T + t];
     } else {
@@ -890,11 +924,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
           // the lattice point times conj(Hhat w), w = 1 / ||Hhat|| / sqrt(F): vk accumulates
           // |Hhat w|^2 = |Hhat|^2 / ||Hhat||^2 / F directly (11 f64 ops per slot, not 13;
           // vk_scale restores the factor F)
-          uint32_t l = slab(s);
           R in = inv_nrm[s];
-          asm volatile("" : "+v"(l), "+v"(in));
+          asm volatile("" : "+v"(in));
           const C ew = cscale(e, in * inv_sqrt_f);
-          x[s] = cmulc(levels_point<R>(l), ew);
+          x[s] = cmulc(slab_point(s), ew);
           vk = fmar(ew.x, ew.x, fmar(ew.y, ew.y, vk));
         } else {
           x[s] = cmulc(symw(s), e);  // s conj(Hhat) / ||Hhat|| / sqrt(F); 0 off band (symw = 0)
