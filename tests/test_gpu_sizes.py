@@ -26,11 +26,17 @@ CASES = [
     (512, 256, 16, 4, "toi", 0.0, 5.0, None),        # QPSK, cubic PA
     (2048, 1024, 8, 256, "softlim", 0.0, 0.0, None),  # 256-QAM at IBO 0 (strong clipping)
     (128, 4, 2, 16, "softlim", 0.0, -2.0, None),     # smallest band (4 sub-carriers), deep clipping
+    # 2 antennas on 4-8 sub-carriers: the per-antenna precoding power strays far outside the
+    # alpha fit's |x| <= 0.25, so the fallback runs (alpha_fit.h segment table at F 2048 /
+    # 8192, the inline library form at F 4096)
+    (2048, 8, 2, 16, "softlim", 0.0, 1.0, None),
+    (4096, 8, 2, 16, "softlim", 0.0, 1.0, None),
+    (8192, 4, 2, 16, "softlim", 0.0, 1.0, None),
     (256, 252, 4, 16, "softlim", 0.0, 2.0, None),    # widest band allowed (S = F - 4)
     (256, 128, 2048, 64, "softlim", 0.0, 0.0, None),  # many antennas
     (1024, 512, 1, 1024, "softlim", 0.0, 100.0, None),  # SISO, ideal PA, 1024-QAM
 ]
-EBN0 = {(128, 4): 6.0, (256, 128): 8.0, (1024, 512): 30.0}
+EBN0 = {(128, 4): 6.0, (256, 128): 8.0, (1024, 512): 30.0, (2048, 8): 8.0, (4096, 8): 8.0, (8192, 4): 8.0}
 
 
 @pytest.mark.parametrize("prec", PRECISIONS)
