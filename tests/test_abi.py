@@ -142,3 +142,14 @@ def test_precision_selects_the_instance(prec, team):
     assert desc.startswith("F=2048 T=256" if prec == 0 else "F=2048 T=128"), desc
     assert desc.endswith("f64" if prec == 0 else "f32"), desc
     lib.mimo_engine_destroy(h)
+
+
+def test_calc_alpha_validates_without_a_gpu():
+    """mimo_calc_alpha (ABI 6): an empty request succeeds and a negative count is rejected
+    host-side, before any HIP call."""
+    lib = _engine.lib()
+    out = np.zeros(1)
+    dp = ctypes.POINTER(ctypes.c_double)
+    assert lib.mimo_calc_alpha(out.ctypes.data_as(dp), 0, out.ctypes.data_as(dp)) == 0
+    assert lib.mimo_calc_alpha(out.ctypes.data_as(dp), -1, out.ctypes.data_as(dp)) == -1  # MIMO_EINVAL
+    assert "n < 0" in lib.mimo_last_error().decode()
