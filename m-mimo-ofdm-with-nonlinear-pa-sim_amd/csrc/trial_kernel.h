@@ -520,6 +520,49 @@ struct Channel {
     }
   }
 
+  // |H|^2 of antenna a at the thread's slots for the closed-form channels (gen<false>'s
+  // magnitudes, for pass 1's MRT norms): LoS |a1 e^{j phi1}|^2 = a1^2 -- no phase at all;
+  // two-path |a1 e^{j phi1} - a2 e^{j phi2}|^2 = a1^2 + a2^2 - 2 a1 a2 cos(phi1 - phi2) --
+  // one cosine of the path difference instead of two sine / cosine pairs.
+  template <class PP>
+  static __device__ __forceinline__ void power_closed(const PP& p, int a, int t, const double (&rx)[3],
+                                                      R (&e2)[NSLOT]) {
+    static_assert(CH == CH_LOS || CH == CH_TWOPATH, "closed-form channels");
+    const int S = p.n_sc;
+    const double tx = p.tx_pos[3 * a], ty = p.tx_pos[3 * a + 1], tz = p.tx_pos[3 * a + 2];
+    const double dx = tx - rx[0], dy = ty - rx[1], dz = tz - rx[2];
+    const double d_los = sqrt(dx * dx + dy * dy + dz * dz);
+    const R att_los = (R)(p.d0 / d_los);
+    if constexpr (CH == CH_LOS) {
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) {
+        bool v;
+        SL::k_of(s, t, S, v);
+        e2[s] = v ? att_los * att_los : R(0);
+      }
+    } else {
+      const double hz = tz + rx[2];
+      const double d_sec = sqrt(dx * dx + dy * dy + hz * hz);
+      const R att_sec = (R)(p.d0 / d_sec);
+      const R a11 = fmar(att_los, att_los, att_sec * att_sec), a12 = R(2) * att_los * att_sec;
+      const double dd = d_los - d_sec;
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) {
+        bool v;
+        const int k = SL::k_of(s, t, S, v);
+        R e = R(0);
+        if (v) {
+          double ph = dd * p.f_over_c[k];
+          ph -= floor(ph);
+          R sn, cs;
+          sincos_phase((R)ph, sn, cs);
+          e = fmar(-a12, cs, a11);
+        }
+        e2[s] = e;
+      }
+    }
+  }
+
   // True channel of antenna a at the thread's slots (relative scale: common factors
   // cancel in MRT, AGC and the SNR normalisation).  FREL = false leaves out the
   // per-sub-carrier FSPL factor fc/f_k, which the kernel then applies once per trial
@@ -732,6 +775,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         for (int s = 0; s < NSLOT; ++s) nrm2[s] += e2[s];
         continue;
       }
+    }
+    if constexpr ((CH == CH_LOS || CH == CH_TWOPATH) && !CSI) {
+      R e2[NSLOT];
+      CHN::power_closed(p, a, tl, rx, e2);
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) nrm2[s] += e2[s];
+      continue;
     }
     C h[NSLOT];
     CHN::template gen<FREL>(p, key, ch_trial, a, tl, rx, h);
