@@ -307,3 +307,21 @@ def test_multi_user_is_rejected_explicitly():
     h = link.my_miso_chan.channel_mat_fd
     with pytest.raises(NotImplementedError):
         link.my_array.set_precoding_matrix([h, h], mr_precoding=True)
+
+
+def test_next_batch_rows_equals_next_batch():
+    """simulate_points' vectorised stopping rule gives every point exactly next_batch's batch
+    (pilot, doubling, rate-based need, bit budget, max_batch), including closed counters,
+    zero-error and zero-bit counters."""
+    import mp_model
+    rng = np.random.default_rng(5)
+    nbps, nmin, bmax = 12288, 100000, 5_000_000
+    for trial in range(200):
+        P, n_idx = 37, 5
+        bits = rng.choice([0.0, 12288.0 * 64, 12288.0 * 300, 4.99e6, 5.0e6, 6e6], size=(P, n_idx))
+        err = np.where(rng.random((P, n_idx)) < 0.2, 0.0, np.floor(bits * rng.choice([1e-4, 1e-2, 0.05, 0.3], (P, n_idx))))
+        act = (err < nmin) & (bits < bmax)
+        got = mp_model.next_batch_rows(err, bits, act, nbps, nmin, bmax, 65536)
+        for i in range(P):
+            if act[i].any():
+                assert got[i] == mp_model.next_batch(err[i], bits[i], act[i], nbps, nmin, bmax, 65536), (i, err[i], bits[i])
