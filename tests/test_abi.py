@@ -33,6 +33,13 @@ def test_library_exports_every_declared_symbol():
     assert lib.mimo_abi_version() == 6
 
 
+def test_build_entry_checks_the_header_abi():
+    """__graft_entry__.build() compares the library's ABI with include/mimo_engine.h's
+    MIMO_ABI_VERSION (a hard-coded number there went stale once: ABI 5 -> 6)."""
+    import __graft_entry__ as g
+    assert g._header_abi_version() == _engine.lib().mimo_abi_version() == 6
+
+
 def _cfg(**kw):
     tx = np.zeros((kw.get("n_ant", 4), 3))
     fr = np.full(kw.get("n_fft", 256), 3.5e9)
