@@ -87,3 +87,38 @@ def test_config5_array_vs_oracle(A, M, pa, p, ibo, channel, receiver, n, prec):
     _, _, per = eng.run(77, 0, n, iters, True, per_trial=True)
     print("config5", A, M, pa, channel, receiver, eng.describe(), per.sum(0), ref.sum(0))
     assert_counts_equal(per, ref, f"config5 {A}/{M}/{pa}/{channel}/{receiver} {prec}")
+
+
+BENCH_GEOMETRIES = [
+    # F,    S,    channel,    receiver, csi
+    (2048, 1024, "los", "cnc", None),
+    (2048, 1024, "two_path", "cnc", None),
+    (2048, 1024, "rayleigh", "cnc", 0.1),
+    (2048, 1024, "rayleigh", "mcnc", None),
+    (4096, 2048, "los", "cnc", None),
+    (4096, 2048, "two_path", "cnc", None),
+    (4096, 2048, "rayleigh", "cnc", 0.1),
+    (4096, 2048, "rayleigh", "mcnc", None),
+    (4096, 2048, "two_path", "mcnc", None),
+]
+
+
+@pytest.mark.parametrize("prec", PRECISIONS)
+@pytest.mark.parametrize("F,S,channel,receiver,csi", BENCH_GEOMETRIES)
+def test_bench_line_instances_vs_oracle(F, S, channel, receiver, csi, prec):
+    """The kernel instances behind bench.py's secondary lines (config-2 geometry F 2048 and
+    the paper geometry F 4096: LoS, two-path, CSI error, MCNC) at 8 antennas: per-trial
+    counts EXACTLY equal to the oracle's.  The antenna count does not select the instance
+    (F, S, channel, CSI do), so these are the instances the 64-antenna lines time, including
+    the closed-form pass-1 powers of LoS / two-path (round 4)."""
+    A, M = 8, 64
+    snr = float(sim.rm.ebn0_to_snr(12.0, S, S, M))
+    cfg = sim.SimConfig(A, S, F, M, pa="softlim", ibo_db=2.0, snr_db=snr, channel=channel, receiver=receiver,
+                        csi_eps=csi)
+    iters = [0, 1, 2]
+    n = 6
+    ref = sim.run_trials(cfg, 4242, np.arange(n), iters=iters, incl_clean=True, chunk=2)
+    eng = engine_for(cfg, precision=prec)
+    _, _, per = eng.run(4242, 0, n, iters, True, per_trial=True)
+    print("bench-line instance", F, S, channel, receiver, csi, eng.describe(), per.sum(0), ref.sum(0))
+    assert_counts_equal(per, ref, f"{F}/{S}/{channel}/{receiver}/csi={csi} {prec}")
