@@ -122,3 +122,33 @@ def test_bench_line_instances_vs_oracle(F, S, channel, receiver, csi, prec):
     _, _, per = eng.run(4242, 0, n, iters, True, per_trial=True)
     print("bench-line instance", F, S, channel, receiver, csi, eng.describe(), per.sum(0), ref.sum(0))
     assert_counts_equal(per, ref, f"{F}/{S}/{channel}/{receiver}/csi={csi} {prec}")
+
+
+PA_PATHS = [
+    # F,    S,    pa,     p     (Rayleigh, CNC)
+    (2048, 1024, "rapp", 3.0),   # integer-hardness Rapp (rapp_int<3>)
+    (2048, 1024, "rapp", 2.0),   # rapp_int<2>
+    (2048, 1024, "rapp", 2.5),   # general p: out of line at F 2048 (pa_rapp_general)
+    (2048, 1024, "toi", 0.0),
+    (4096, 2048, "rapp", 3.0),
+    (4096, 2048, "rapp", 2.5),   # general p: inline at F 4096 (COLD_OUT off)
+    (4096, 2048, "toi", 0.0),
+]
+
+
+@pytest.mark.parametrize("prec", PRECISIONS)
+@pytest.mark.parametrize("F,S,pa,p", PA_PATHS)
+def test_pa_paths_per_instance_vs_oracle(F, S, pa, p, prec):
+    """Every PA branch of pa_block() in the F 2048 and F 4096 instances (the PA kind is a
+    run-time switch inside one instance, and the general-p Rapp is out of line at F 2048 but
+    inline at F 4096): per-trial counts EXACTLY equal to the oracle's."""
+    A, M = 8, 64
+    snr = float(sim.rm.ebn0_to_snr(12.0, S, S, M))
+    cfg = sim.SimConfig(A, S, F, M, pa=pa, p_hardness=p, ibo_db=1.5, snr_db=snr)
+    iters = [0, 1, 2]
+    n = 6
+    ref = sim.run_trials(cfg, 515, np.arange(n), iters=iters, incl_clean=True, chunk=2)
+    eng = engine_for(cfg, precision=prec)
+    _, _, per = eng.run(515, 0, n, iters, True, per_trial=True)
+    print("pa path", F, S, pa, p, eng.describe(), per.sum(0), ref.sum(0))
+    assert_counts_equal(per, ref, f"{F}/{S}/{pa}/{p} {prec}")
