@@ -248,8 +248,9 @@ def time_grid(rank, world, dist, dev, precision, tdev, fake=False):
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
+    st = {}
     err, bits = sweep.run_grid(link, c4["ibo"], c4["ebn0"], c4["iters"], incl_clean=False, seed=2137, rank=rank,
-                               world=world, dist=dist, device=dev)
+                               world=world, dist=dist, device=dev, stats=st)
     if not fake:
         import torch
         torch.cuda.synchronize()
@@ -257,23 +258,38 @@ def time_grid(rank, world, dist, dev, precision, tdev, fake=False):
         dist.barrier()
     dt = time.perf_counter() - t0
     ranks = 1
+    mine = {k: st[k] for k in ("rank", "points", "trials", "rounds", "kernel_ms", "wall_s")}
+    mine["cost_model"] = round(float(np.sum(st["cost_model"])), 1)
+    per_rank = [mine]
     if dist:
         import torch
         t = torch.tensor([dt, 1.0], device=tdev, dtype=torch.float64)
         dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:])
         dt, ranks = float(t[0].item()), int(t[1].item())
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     m = link.my_mod
     bits_per_sym = int(m.n_sub_carr * np.log2(m.constel_size))
-    n_sym = int(bits[..., 0].sum()) // bits_per_sym
+    # OFDM symbols run: every counter of a point shares its trials, and the counter that stayed
+    # open longest saw them all (iteration 0 closes first in a fixed-BER grid)
+    n_sym = int(bits.max(axis=-1).sum()) // bits_per_sym
     digest = hashlib.sha256(np.ascontiguousarray(err, np.int64).tobytes() +
                             np.ascontiguousarray(bits, np.int64).tobytes()).hexdigest()[:16]
-    return {"workload": "BASELINE config 4: Eb/N0 0-30 dB x IBO 0-7 dB (0.5 dB steps), CNC iterations 0-8, "
+    loads = [r["trials"] for r in per_rank]
+    costs = [r["cost_model"] for r in per_rank]
+    return {"workload": "BASELINE config 4: Eb/N0 0-30 dB x IBO 0-7 dB (0.5 dB steps; Eb/N0 is the swept axis), "
+                        "CNC iterations 0-8, "
                         "bits_sent_max 5e6 / n_err_min 1e5 per point, 64-ant / FFT 4096 / 2048-sc paper geometry"
                         + (" [CPU rehearsal: stand-in link]" if fake else ""),
+            "axis": "Eb/N0 (the drivers' axis, main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:103-112; "
+                    "BASELINE's 'SNR 0-30 dB' read as Eb/N0: SNR = Eb/N0 + 7.8 dB at 64-QAM)",
             "points": int(len(c4["ibo"]) * len(c4["ebn0"])), "ofdm_symbols": n_sym, "wall_s": round(dt, 4),
             "symbols_per_s": round(n_sym / dt, 1), "ranks_seen": ranks, "scaling": "strong",
             "parallelism": f"points dealt by cost (LPT) over {world} rank(s), one all-reduce of the counters",
+            "per_rank": per_rank,
+            "trials_max_over_mean": round(max(loads) / max(1e-9, float(np.mean(loads))), 4),
+            "model_max_over_mean": round(max(costs) / max(1e-9, float(np.mean(costs))), 4),
             "counts_digest": digest}
 
 
@@ -321,7 +337,7 @@ def main():
     if args.grid_check:  # CPU rehearsal of the grid line: gloo ranks, stand-in link, no GPU
         import torch.distributed as gdist
         gd = None
-        if world > 1:
+        if "WORLD_SIZE" in os.environ:
             gdist.init_process_group("gloo")
             gd = gdist
         g = time_grid(rank, world, gd, None, args.precision, "cpu", fake=True)
@@ -337,7 +353,9 @@ def main():
     backend = os.environ.get("MIMO_BENCH_BACKEND", "nccl")
     dev = local % max(1, torch.cuda.device_count())
     tdev = f"cuda:{dev}" if backend == "nccl" else "cpu"
-    if world > 1:
+    # A process group whenever a launcher started this rank (torchrun sets WORLD_SIZE), also at
+    # world size 1: the RCCL code path of the N-GPU runs is then the one every run takes.
+    if "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
         torch.cuda.set_device(dev)
         dist.init_process_group(backend)

@@ -24,6 +24,7 @@
  *     mimo_awgn                 <- Awgn.process                        noise.py:45-83
  *     mimo_count_bit_errors     <- utilities.count_mismatched_bits     utilities.py:94-104
  *     mimo_cnc_receive          <- CncReceiver.receive                 corrector.py:52-112
+ *     mimo_cnc_receive_ex       <- CncReceiver.receive(return_bits=False) corrector.py:80-84
  *
  * Conventions: complex arrays are interleaved (re, im) doubles; sizes are element
  * counts; functions return 0 on success and a negative MIMO_E* code on error, with a
@@ -40,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MIMO_ABI_VERSION 6
+#define MIMO_ABI_VERSION 7
 
 enum { MIMO_OK = 0, MIMO_EINVAL = -1, MIMO_EHIP = -2, MIMO_ENOKERNEL = -3, MIMO_ENOMEM = -4 };
 enum { MIMO_PA_NONE = 0, MIMO_PA_SOFTLIM = 1, MIMO_PA_RAPP = 2, MIMO_PA_TOI = 3 };
@@ -78,7 +79,7 @@ typedef struct mimo_config {
                                curves' channel variance (tests/test_gpu_link.py).  (ABI 5) */
   uint64_t csi_seed;        /* MIMO_CH_TABLE with CSI error: Philox key of the one erroneous
                                estimate every trial and every run shares -- Link.__init__ draws it
-                               once from its own CSI noise generator (mp_model.py:76-87), so the
+                               once from its noise generator, default_rng(0) (mp_model.py:74,87,272), so the
                                workers of a point see the same estimate whatever their seeds.
                                0: the run's seed (ABI 5 behaviour).  (ABI 6) */
 } mimo_config;
@@ -153,6 +154,13 @@ int32_t mimo_count_bit_errors(const int64_t* a, const int64_t* b, int64_t n, int
 int32_t mimo_cnc_receive(int32_t constel_size, int32_t n_fft, int32_t n_sub_carr, int32_t pa_kind, double sat_pow,
                          double p_hardness, double toi_coeff, double alpha, const int32_t* iters, int32_t n_iters,
                          const double* in_sc_iq, int32_t* labels_out);
+/* ABI 7: the same loop with optional outputs -- labels_out [n_iters][S] and/or
+ * corrected_iq_out [n_iters][S] (re, im), the slicer input rx - d of each listed iteration,
+ * which CncReceiver.receive(return_bits=False) returns (corrector.py:80-84).  Either may be
+ * null. */
+int32_t mimo_cnc_receive_ex(int32_t constel_size, int32_t n_fft, int32_t n_sub_carr, int32_t pa_kind, double sat_pow,
+                            double p_hardness, double toi_coeff, double alpha, const int32_t* iters, int32_t n_iters,
+                            const double* in_sc_iq, int32_t* labels_out, double* corrected_iq_out);
 
 #ifdef __cplusplus
 }

@@ -81,6 +81,9 @@ SYMBOLS = {
     "mimo_cnc_receive": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                           ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, _i32p,
                                           ctypes.c_int32, _dp, _i32p]),
+    "mimo_cnc_receive_ex": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, _i32p,
+                                             ctypes.c_int32, _dp, _i32p, _dp]),
 }
 
 _lib = None
@@ -341,12 +344,19 @@ def count_bit_errors(a, b):
     return int(out[0])
 
 
-def cnc_receive(constel_size, n_fft, pa_kind, sat_pow, p_hardness, toi_coeff, alpha, iters, rx_sc):
+def cnc_receive(constel_size, n_fft, pa_kind, sat_pow, p_hardness, toi_coeff, alpha, iters, rx_sc, return_bits=True):
+    """{iteration: detected labels}, or with ``return_bits=False`` {iteration: the corrected
+    slicer input rx - d} (mimo_cnc_receive_ex)."""
     z = as_iq(np.asarray(rx_sc).reshape(-1))
     S = z.size // 2
     it = _c(sorted(set(int(i) for i in iters)), np.int32)
-    out = np.empty((len(it), S), np.int32)
-    _check(lib().mimo_cnc_receive(int(constel_size), int(n_fft), S, PA_KINDS[pa_kind], float(sat_pow),
-                                  float(p_hardness), float(toi_coeff), float(alpha), _ptr(it, ctypes.c_int32), len(it),
-                                  _ptr(z, ctypes.c_double), _ptr(out, ctypes.c_int32)))
-    return {int(i): out[j].astype(np.int64) for j, i in enumerate(it)}
+    lab = np.empty((len(it), S), np.int32) if return_bits else None
+    cor = None if return_bits else np.empty((len(it), S), np.complex128)
+    _check(lib().mimo_cnc_receive_ex(int(constel_size), int(n_fft), S, PA_KINDS[pa_kind], float(sat_pow),
+                                     float(p_hardness), float(toi_coeff), float(alpha), _ptr(it, ctypes.c_int32),
+                                     len(it), _ptr(z, ctypes.c_double),
+                                     _ptr(lab, ctypes.c_int32) if lab is not None else None,
+                                     _ptr(cor.view(np.float64), ctypes.c_double) if cor is not None else None))
+    if return_bits:
+        return {int(i): lab[j].astype(np.int64) for j, i in enumerate(it)}
+    return {int(i): cor[j] for j, i in enumerate(it)}

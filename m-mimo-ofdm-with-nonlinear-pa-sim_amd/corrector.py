@@ -44,13 +44,14 @@ class CncReceiver:
         alpha = self.modem.alpha if alpha_estimate is None else alpha_estimate
         kind, sat, p, toi = distortion.pa_params(self.impairment)
         iters = sorted(set(int(i) for i in np.atleast_1d(n_iters_lst)))
-        if not return_bits:
-            raise NotImplementedError("return_bits=False is not supported by the GPU CNC stage")
         s = _qam_scale(self.modem.constellation)
-        labs = _engine.cnc_receive(self.modem.constel_size, self.modem.n_fft, kind, sat, p, toi, alpha, iters,
-                                   rx / s if s != 1.0 else rx)
+        out = _engine.cnc_receive(self.modem.constel_size, self.modem.n_fft, kind, sat, p, toi, alpha, iters,
+                                  rx / s if s != 1.0 else rx, return_bits=return_bits)
+        if not return_bits:
+            # the corrected in-band symbols the slicer saw (corrector.py:80-84), in the caller's scale
+            return [out[i] * s if s != 1.0 else out[i] for i in iters]
         from utilities import dec2bitarray
-        return [dec2bitarray(labs[i], self.modem.n_bits_per_symbol) for i in iters]
+        return [dec2bitarray(out[i], self.modem.n_bits_per_symbol) for i in iters]
 
 
 class McncReceiver:

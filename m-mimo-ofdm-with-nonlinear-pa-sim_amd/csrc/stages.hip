@@ -441,10 +441,12 @@ int32_t mimo_count_bit_errors(const int64_t* a, const int64_t* b, int64_t n, int
 }
 
 // CncReceiver.receive (corrector.py:52-112) for one in-band vector; labels_out is
-// [n_iters][S] (the iterations listed, ascending).
-int32_t mimo_cnc_receive(int32_t M, int32_t F, int32_t S, int32_t pa_kind, double sat, double p, double toi,
-                         double alpha, const int32_t* iters, int32_t n_iters, const double* in_sc_iq,
-                         int32_t* labels_out) {
+// [n_iters][S] (the iterations listed, ascending); corrected_iq_out (return_bits=False,
+// corrector.py:80-84) the slicer's input rx - d of those iterations, [n_iters][S] (re, im).
+// Either output may be null.
+int32_t mimo_cnc_receive_ex(int32_t M, int32_t F, int32_t S, int32_t pa_kind, double sat, double p, double toi,
+                            double alpha, const int32_t* iters, int32_t n_iters, const double* in_sc_iq,
+                            int32_t* labels_out, double* corrected_iq_out) {
   const int L = qam_l(M);
   if (!L) return sfail(MIMO_EINVAL, "Constellation size must be a power of some number, only square QAM supported.");
   if (n_iters < 1) return sfail(MIMO_EINVAL, "empty iteration list");
@@ -472,7 +474,10 @@ int32_t mimo_cnc_receive(int32_t M, int32_t F, int32_t S, int32_t pa_kind, doubl
     hipLaunchKernelGGL(k_qam_slice, grid_for(S), dim3(256), 0, 0, L, hb, dv.as<double2>(), (int64_t)S, dlab.as<int32_t>());
     S_TRY(hipGetLastError());
     if (out_i < n_iters && iters[out_i] == it) {
-      S_TRY(hipMemcpy(labels_out + (size_t)out_i * S, dlab.p, S * sizeof(int32_t), hipMemcpyDeviceToHost));
+      if (labels_out)
+        S_TRY(hipMemcpy(labels_out + (size_t)out_i * S, dlab.p, S * sizeof(int32_t), hipMemcpyDeviceToHost));
+      if (corrected_iq_out)
+        S_TRY(hipMemcpy(corrected_iq_out + (size_t)out_i * 2 * S, dv.p, S * sizeof(double2), hipMemcpyDeviceToHost));
       ++out_i;
     }
     if (it == max_it) break;
@@ -489,6 +494,13 @@ int32_t mimo_cnc_receive(int32_t M, int32_t F, int32_t S, int32_t pa_kind, doubl
   }
   S_TRY(hipDeviceSynchronize());
   return MIMO_OK;
+}
+
+int32_t mimo_cnc_receive(int32_t M, int32_t F, int32_t S, int32_t pa_kind, double sat, double p, double toi,
+                         double alpha, const int32_t* iters, int32_t n_iters, const double* in_sc_iq,
+                         int32_t* labels_out) {
+  if (!labels_out) return sfail(MIMO_EINVAL, "null labels_out");
+  return mimo_cnc_receive_ex(M, F, S, pa_kind, sat, p, toi, alpha, iters, n_iters, in_sc_iq, labels_out, nullptr);
 }
 
 }  // extern "C"

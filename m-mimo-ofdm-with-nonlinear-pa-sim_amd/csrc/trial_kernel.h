@@ -522,8 +522,12 @@ struct Channel {
 
   // |H|^2 of antenna a at the thread's slots for the closed-form channels (gen<false>'s
   // magnitudes, for pass 1's MRT norms): LoS |a1 e^{j phi1}|^2 = a1^2 -- no phase at all;
-  // two-path |a1 e^{j phi1} - a2 e^{j phi2}|^2 = a1^2 + a2^2 - 2 a1 a2 cos(phi1 - phi2) --
-  // one cosine of the path difference instead of two sine / cosine pairs.
+  // two-path |a1 e^{j phi1} - a2 e^{j phi2}|^2 = (a1 - a2)^2 + 4 a1 a2 sin^2((phi1 - phi2) / 2)
+  // -- one sine of the half path difference instead of two sine / cosine pairs, in the
+  // cancellation-free form: a2 / a1 = d_los / d_sec is within ~1e-3 of 1 for the reference's
+  // geometry, so at a reflection null (aligned across a ULA) the true value sits near
+  // (a1 - a2)^2 ~ 1e-7 a1^2, below the rounding of a1^2 + a2^2 - 2 a1 a2 cos in fp32.  The
+  // difference a1 - a2 is formed in fp64 and the half phase reduced to [-1/4, 1/4] rev first.
   template <class PP>
   static __device__ __forceinline__ void power_closed(const PP& p, int a, int t, const double (&rx)[3],
                                                       R (&e2)[NSLOT]) {
@@ -543,8 +547,10 @@ struct Channel {
     } else {
       const double hz = tz + rx[2];
       const double d_sec = sqrt(dx * dx + dy * dy + hz * hz);
-      const R att_sec = (R)(p.d0 / d_sec);
-      const R a11 = fmar(att_los, att_los, att_sec * att_sec), a12 = R(2) * att_los * att_sec;
+      const double g_sec = p.d0 / d_sec;
+      const R d12 = (R)(p.d0 / d_los - g_sec);
+      const R a4 = R(4) * att_los * (R)g_sec;
+      const R d12sq = d12 * d12;
       const double dd = d_los - d_sec;
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
@@ -553,10 +559,10 @@ struct Channel {
         R e = R(0);
         if (v) {
           double ph = dd * p.f_over_c[k];
-          ph -= floor(ph);
+          ph -= rint(ph);  // [-1/2, 1/2] rev: the half phase keeps its relative precision
           R sn, cs;
-          sincos_phase((R)ph, sn, cs);
-          e = fmar(-a12, cs, a11);
+          sincos_phase((R)(0.5 * ph), sn, cs);
+          e = fmar(a4 * sn, sn, d12sq);
         }
         e2[s] = e;
       }

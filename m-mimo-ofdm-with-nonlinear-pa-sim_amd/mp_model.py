@@ -244,10 +244,12 @@ class Link:
         self.loc_rng = np.random.default_rng(1)
         self.bit_rng = np.random.default_rng(2)
         self.my_csi_noise.rng_gen = np.random.default_rng(3)
-        # the fixed-channel (reroll_chan=False) CSI estimate is the Link's, drawn once from its
-        # own CSI generator (seed 3 above, mp_model.py:76-87): its Philox key, shared by every
-        # worker and every simulate() call whatever their seed_arr
-        self.csi_seed = _seed64([3, 0xC51])
+        # the fixed-channel (reroll_chan=False) CSI estimate is the Link's: Link.__init__ draws
+        # it once, in set_precoding_and_recalculate_agc, from self.my_noise.rng_gen, which it
+        # has just seeded with default_rng(0) (mp_model.py:74,87,272 -- not my_csi_noise, seed
+        # 3, which the reference never draws from).  Its Philox key (0 as in that seed, 0xC51 a
+        # stream tag), shared by every worker and every simulate() call whatever their seed_arr
+        self.csi_seed = _seed64([0, 0xC51])
         self.rx_loc_var = rx_loc_var
         self.n_ant_val = len(self.my_array.array_elements)
         self.n_bits_per_ofdm_sym = self.my_mod.n_bits_per_ofdm_sym
@@ -383,14 +385,15 @@ class Link:
                     lock.release()
 
     def simulate_points(self, incl_clean_run: bool, reroll_chan: bool, cnc_n_iter_lst, seed_arrs, point_params,
-                        n_err, n_bits) -> None:
+                        n_err, n_bits, stats: dict = None) -> None:
         """``simulate`` for many grid points of this system at once (the drivers' grid loops,
         main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:100-215): every round launches one
         batch of every still-open point (mimo_engine_run_points); the counters of point i
         (``n_err[i]``, ``n_bits[i]``: float arrays [n_idx], added to) follow the same stopping
         rule and batch sizes as ``simulate`` would give them, so the totals are bit-identical.
         ``point_params[i]`` is ``point_params()`` captured at point i (after
-        update_distortion / set_snr)."""
+        update_distortion / set_snr).  ``stats`` (a dict, optional) receives the work record:
+        ``trials`` per point, and per round the open points, trials and kernel ms."""
         eng = self.engine(reroll_chan)
         P = len(point_params)
         iters_all = np.asarray(cnc_n_iter_lst, dtype=np.int64).reshape(-1)
@@ -414,6 +417,7 @@ class Link:
         # spent ~50 ms per round in per-point Python otherwise)
         mpoints = [_engine.Engine.make_point(**pp) for pp in point_params]
         seeds_a = np.asarray([s & 0xFFFFFFFFFFFFFFFF for s in seeds], dtype=np.uint64)
+        rounds = []
         while True:
             act = (n_err < self.n_err_min) & (n_bits < self.bits_sent_max)
             rows = np.flatnonzero(act.any(axis=1))
@@ -423,6 +427,8 @@ class Link:
                                 self.bits_sent_max, self.max_batch)
             t0 = time.perf_counter()
             e, b, _ = eng.run_points([mpoints[i] for i in rows], seeds_a[rows], trial[rows], n, uniq, incl_clean_run)
+            rounds.append(dict(points=int(rows.size), trials=int(n.sum()), kernel_ms=round(float(eng.kernel_ms), 3),
+                               call_ms=round(1e3 * (time.perf_counter() - t0), 3)))
             if os.environ.get("MIMO_SWEEP_TRACE"):
                 import sys
                 print("simulate_points round: %d points, %d trials, kernel %.2f ms, call %.2f ms"
@@ -431,6 +437,8 @@ class Link:
             n_err[rows] += np.where(a, e[:, col].astype(np.float64), 0.0)
             n_bits[rows] += np.where(a, b[:, col].astype(np.float64), 0.0)
             trial[rows] += n
+        if stats is not None:
+            stats.update(trials=trial.copy(), rounds=rounds)
 
     def update_distortion(self, ibo_val_db: float) -> None:
         """(mp_model.py:230-241)"""

@@ -32,6 +32,12 @@ from utilities import ebn0_to_snr, save_to_csv
 # 0..30 dB x IBO 0..7 dB in 0.5 dB steps = 915 points, receiver iterations 0..8, the fixed-BER
 # driver's stopping rule and geometry (main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:40-61,
 # 100-215: 64-antenna ULA, FFT 4096, 2048 sub-carriers, 64-QAM, soft limiter).
+# The swept axis is Eb/N0, the drivers' own axis (main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:
+# 103-112 sweep ebn0_db_arr and convert with ebn0_to_snr), not the SNR that BASELINE.json names:
+# "0-30 dB" is read as Eb/N0 0-30 dB, i.e. SNR = Eb/N0 + 10 log10(6) = 7.8-37.8 dB at 64-QAM.
+# (A literal SNR 0-30 dB grid is Eb/N0 -7.8..22.2 dB: more low-SNR points that close on
+# n_err_min within a few dozen trials, fewer capped at the bit budget -- a cheaper grid.)
+# bench.py's grid object names the axis.
 BASELINE_C4 = dict(ibo=np.arange(0.0, 7.01, 0.5), ebn0=np.arange(0.0, 30.01, 0.5), iters=np.arange(0, 9),
                    n_ant=64, n_sc=2048, n_fft=4096, qam=64, cp=128, bits_sent_max=int(5e6), n_err_min=int(1e5))
 
@@ -113,13 +119,17 @@ def point_costs(ibo_arr, ebn0_arr, n_bits_per_sym, constel_size, n_err_min, bits
 
 
 def run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean=True, seed=2137, rank=0, world=1, dist=None,
-             device=None, reroll_chan=True, multipoint=True):
+             device=None, reroll_chan=True, multipoint=True, stats=None):
     """Simulate every (IBO, Eb/N0) point this rank owns; all-reduce the counters.
 
     Returns (err, bits) int64 arrays of shape [n_ibo, n_ebn0, n_idx] on every rank.
     ``link`` is a ``mp_model.Link``-like object (update_distortion / set_snr / simulate;
     with ``simulate_points`` all owned points run together, a few launches per grid).
-    Points are dealt by estimated cost (``point_costs``, LPT).
+    Points are dealt by estimated cost (``point_costs``, LPT).  ``stats`` (a dict, optional)
+    receives this rank's work record: its points, their modelled costs and trials run, the
+    stopping-rule rounds with their kernel ms, and the wall time of its share (before the
+    all-reduce).  With a process group (``dist``), the counters are all-reduced even at
+    world size 1 (one code path for every N).
     """
     ibo_arr = np.asarray(ibo_arr, dtype=np.float64)
     ebn0_arr = np.asarray(ebn0_arr, dtype=np.float64)
@@ -133,6 +143,8 @@ def run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean=True, seed=2137, rank=0,
                         getattr(link, "bits_sent_max", 5e6), iters, getattr(link, "n_ant_val", 64),
                         getattr(link, "is_mcnc", False))
     mine = owned_points(n_pts, rank, world, costs)
+    t_start = time.perf_counter()
+    sim_stats = {}
     batched = multipoint and hasattr(link, "simulate_points")
     current_ibo = None
     params, seeds = [], []
@@ -155,14 +167,27 @@ def run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean=True, seed=2137, rank=0,
     if batched and mine:
         err = np.zeros((len(mine), n_idx))
         bits = np.zeros((len(mine), n_idx))
-        link.simulate_points(incl_clean, reroll_chan, iters, seeds, params, err, bits)
+        if stats is not None:
+            link.simulate_points(incl_clean, reroll_chan, iters, seeds, params, err, bits, stats=sim_stats)
+        else:
+            link.simulate_points(incl_clean, reroll_chan, iters, seeds, params, err, bits)
         counts[mine, :, 0] = err.astype(np.int64)
         counts[mine, :, 1] = bits.astype(np.int64)
-    if dist is not None and world > 1:
+    if stats is not None:
+        # trials per point: all counters of a point share its trials; the longest-open one has
+        # seen them all (bits / bits per symbol), also without simulate_points' record
+        trials = np.asarray(sim_stats.get("trials", counts[mine, :, 1].max(axis=1) // max(1, n_bits_sym)))
+        rounds = sim_stats.get("rounds", [])
+        stats.update(rank=int(rank), points=len(mine), point_ids=[int(p) for p in mine],
+                     cost_model=[float(costs[p]) for p in mine], trials_per_point=[int(x) for x in trials],
+                     trials=int(np.sum(trials)), rounds=len(rounds),
+                     kernel_ms=round(float(sum(r["kernel_ms"] for r in rounds)), 3), round_log=rounds,
+                     wall_s=round(time.perf_counter() - t_start, 4))
+    if dist is not None:
         import torch
         dev = torch.device(f"cuda:{device}") if device is not None and dist.get_backend() == "nccl" else None
         t = torch.from_numpy(counts).to(dev) if dev is not None else torch.from_numpy(counts)
-        dist.all_reduce(t)  # each point is filled by exactly one rank: SUM == gather
+        dist.all_reduce(t)  # each point is filled by exactly one rank: SUM == gather (world 1: identity)
         counts = t.cpu().numpy()
     counts = counts.reshape(len(ibo_arr), len(ebn0_arr), n_idx, 2)
     return counts[..., 0], counts[..., 1]

@@ -305,10 +305,12 @@ def ula_positions(n_elements, center_freq, wav_len_spacing=0.5, cord_z=0.0):
 
 
 # --------------------------------------------------------------------------- receivers
-def cnc_receive(n_iters_lst, rx_nsc, constellation, n_fft, pa_kind, sat, p_hardness, coeff, alpha):
+def cnc_receive(n_iters_lst, rx_nsc, constellation, n_fft, pa_kind, sat, p_hardness, coeff, alpha,
+                return_bits=True):
     """``CncReceiver.receive`` (corrector.py:52-112) on the in-band vector ``rx_nsc`` [S].
 
-    Returns {iteration: detected labels}.
+    Returns {iteration: detected labels}, or with ``return_bits=False`` {iteration: the
+    corrected input ``rx - d`` the slicer saw} (corrector.py:80-84).
     """
     n_sc = rx_nsc.shape[-1]
     bins = inband_bins(n_fft, n_sc)
@@ -320,7 +322,7 @@ def cnc_receive(n_iters_lst, rx_nsc, constellation, n_fft, pa_kind, sat, p_hardn
         lab = detect_labels(const, v)
         s_hat = const[lab]
         if it in set(int(i) for i in n_iters_lst):
-            out[it] = lab
+            out[it] = lab if return_bits else v
         up = np.zeros(n_fft, dtype=np.complex128)
         up[bins] = s_hat
         td = np.fft.ifft(up, norm="ortho")

@@ -30,14 +30,14 @@ def test_library_exports_every_declared_symbol():
     lib = _engine.lib()
     missing = [n for n in declared_functions() if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.mimo_abi_version() == 6
+    assert lib.mimo_abi_version() == 7
 
 
 def test_build_entry_checks_the_header_abi():
     """__graft_entry__.build() compares the library's ABI with include/mimo_engine.h's
     MIMO_ABI_VERSION (a hard-coded number there went stale once: ABI 5 -> 6)."""
     import __graft_entry__ as g
-    assert g._header_abi_version() == _engine.lib().mimo_abi_version() == 6
+    assert g._header_abi_version() == _engine.lib().mimo_abi_version() == 7
 
 
 def _cfg(**kw):

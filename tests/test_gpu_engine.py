@@ -130,7 +130,7 @@ def test_table_channel_vs_oracle(receiver, csi, prec):
 @pytest.mark.parametrize("prec", PRECISIONS)
 def test_table_channel_csi_estimate_belongs_to_the_link(prec):
     """with a fixed channel the erroneous estimate is the Link's (Link.__init__
-    draws it once, mp_model.py:76-87), not the run's: engines keyed by mimo_config.csi_seed
+    draws it once from my_noise.rng_gen = default_rng(0), mp_model.py:74,87,272), not the run's: engines keyed by mimo_config.csi_seed
     give runs with different seeds (the forked workers of one point) the same estimate --
     each run equals the oracle with the SAME csi_seed and its own run seed, exactly."""
     rng = np.random.default_rng(78)

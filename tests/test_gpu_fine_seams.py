@@ -130,3 +130,28 @@ def test_awgn_power():
     assert np.mean(np.abs(y) ** 2) == pytest.approx(0.2, rel=0.02)
     y2 = n.process(x, avg_sample_pow=2.0)
     assert not np.allclose(y, y2)
+
+
+def test_cnc_receive_corrected_symbols(units):
+    """CncReceiver.receive(return_bits=False) returns, per listed iteration, the corrected
+    in-band symbols the slicer saw, rx - d (corrector.py:80-84), from the GPU CNC stage
+    (mimo_cnc_receive_ex, ABI 7) -- against the oracle's restatement of the same loop."""
+    import distortion
+    from oracle import refmath as rm
+    link, mod = build_link(n_ant=4, n_sc=64, n_fft=128, M=16, ibo=2.0)
+    rx = link.my_cnc_rx
+    iters = list(units["cnc_iters"])
+    got = rx.receive(n_iters_lst=iters, in_sig_fd=units["cnc_in"], return_bits=False)
+    kind, sat, p, toi = distortion.pa_params(rx.impairment)
+    want = rm.cnc_receive(iters, np.asarray(units["cnc_in"])[rm.inband_bins(128, 64)], rm.gray_qam_constellation(16),
+                          128, kind, sat, p, toi, rx.modem.alpha, return_bits=False)
+    assert len(got) == len(sorted(set(iters)))
+    for i, it in enumerate(sorted(set(int(v) for v in iters))):
+        assert got[i].shape == (64,) and np.iscomplexobj(got[i])
+        np.testing.assert_allclose(got[i], want[it], rtol=1e-9, atol=1e-10)
+    # iteration 0 is the received in-band vector itself
+    if 0 in iters:
+        np.testing.assert_allclose(got[0], np.asarray(units["cnc_in"])[rm.inband_bins(128, 64)], rtol=0, atol=0)
+    # and the bits path still agrees with the reference's fixture
+    for i, b in enumerate(rx.receive(n_iters_lst=iters, in_sig_fd=units["cnc_in"])):
+        np.testing.assert_array_equal(b, units["cnc_bits"][i])

@@ -14,6 +14,8 @@
 #                                                      FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic.json
 #   bash tools/gpu.sh test <out> [pytest args]         the GPU suite (or a selection of it)
 #   bash tools/gpu.sh c4 <out> [fixed_ber_check args]  config-4 grids (tools/fixed_ber_check.py)
+#   bash tools/gpu.sh families <out> [family]          published CSI / BER-vs-IBO / small-array curves
+#                                                      (tools/published_families.py)
 set -o pipefail
 export TMPDIR=/tmp
 MODE=$1; O=$2; shift 2
@@ -89,6 +91,10 @@ case $MODE in
   c4)
     timeout -k 10 600 python tools/fixed_ber_check.py "$@" > "$O/c4.json" 2> "$O/c4.err" || exit $?
     cut -c1-400 "$O/c4.json" ;;
+  families)
+    fam=${1:-all}
+    timeout -k 10 900 python -u tools/published_families.py --family $fam --out "$O/families_$fam.json" > "$O/families_$fam.log" 2> "$O/families_$fam.err" || exit $?
+    python -c "import json; [print(d['curve'], d['compared'], d['frac_abs_z_le1'], d['mean_z2'], d['max_abs_z'], d['median_abs_rel'], d['min_p_zero'], d['layout'], {k: v['mean_z2'] for k, v in d.items() if k.startswith('alt_')}) for d in json.load(open('$O/families_$fam.json'))]" ;;
   *)
     echo "unknown mode $MODE"; exit 2 ;;
 esac

@@ -1,0 +1,251 @@
+"""The engine against three more families of BER curves the reference publishes.
+
+Families (CSV data files of figs/csv_results, copied to tests/golden as published_*.csv; row
+layout axis, no-distortion, standard RX, CNC / MCNC iterations 1..8):
+
+* ``csi``   -- BER vs Eb/N0 (5..20 dB, 0.5 dB) with channel-estimation error eps in
+  {0, 0.1, 0.2, 0.3, 0.4}: LoS, 64 antennas, soft limiter at IBO 0 dB, F 4096 / S 2048.
+  Driver main_mp_miso_cnc_csi_err_ber_vs_ebn0.py:41-63,119 (bits_sent_max 3e7, n_err_min
+  1e7) and main_mp_miso_mcnc_csi_err_ber_vs_ebn0.py (n_err_min 1e6).
+* ``ibo``   -- BER vs IBO (0..9 dB, 0.5 dB) at Eb/N0 15 dB and 1000 dB (the noiseless
+  runs), LoS, 64 antennas; plus the Rayleigh / two-path curves at Eb/N0 15 (IBO 0..8.5).
+  Driver main_mp_miso_cnc_ber_vs_ibo.py:41-58,105 (bits_sent_max 1e7, n_err_min 1e5) and
+  main_mp_miso_mcnc_ber_vs_ibo.py (same settings).
+* ``small`` -- BER vs IBO at 1 and 4 antennas (LoS, Rayleigh, two-path), Eb/N0 15.  The
+  same driver with n_ant_arr = [1] / [4] (assumed: the committed driver lists [64]).
+
+The published value's sigma is the spread of the reference's own estimator under its
+stopping rule: every counter stops on its own at n_err_min errors or bits_sent_max bits
+(mp_model.py:137-138,177-187), so counter c of a point averages
+n_c = min(ceil(bits_max / B), ceil(n_err_min / (p_c B))) trials (B = 12,288 bits per OFDM
+symbol, p_c the counter's BER).  Trials are independent (LoS / two-path reroll the RX
+position per trial from each worker's own generator; the Rayleigh workers' shared channel
+sequence changed nothing measurable at 64 antennas, tools/replay_sigma.py), so
+sigma_ref = sd_trial / sqrt(n_c), with sd_trial the per-trial BER spread the engine measures
+at that point.  sigma_gpu = sd_trial / sqrt(n_tr) by the same token.  Compared: points with
+BER >= 1e-5 whose published estimate rests on >= 100 errors.
+
+Zero-region check (the noiseless runs reach BER 0): where the published value is exactly 0,
+the reference saw no erroneous symbol in n_c trials.  With q the fraction of the engine's
+trials that hold any bit error, that has probability (1 - q)^n_c; a point where that is
+below 1e-3 would be a mismatch.
+
+    python tools/published_families.py [--family csi|ibo|small|all] [--out file.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (REPO, os.path.join(REPO, "m-mimo-ofdm-with-nonlinear-pa-sim_amd"), os.path.join(REPO, "tests")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+ITERS = list(range(9))  # standard RX + CNC / MCNC iterations 1..8 (the drivers' cnc_n_iter_lst)
+N_SC, N_FFT, M = 2048, 4096, 64
+BPS = N_SC * 6
+TAIL = "niter1_2_3_4_5_6_7_8"
+
+
+def _curves():
+    out = []
+    for rx, n_err in (("cnc", 1e7), ("mcnc", 1e6)):
+        for eps in (0.0, 0.1, 0.2, 0.3, 0.4):
+            out.append(dict(family="csi", receiver=rx, channel="los", n_ant=64, axis="ebn0", ibo=0.0, eps=eps,
+                            bits_max=3e7, n_err_min=n_err,
+                            file="ber_vs_ebn0_%s_los_csi_eps%1.3f_nant64_ibo0_ebn0_min5_max20_step0.50_%s" % (rx, eps, TAIL)))
+    for rx in ("cnc", "mcnc"):
+        for ebn0 in (15, 1000):
+            out.append(dict(family="ibo", receiver=rx, channel="los", n_ant=64, axis="ibo", ebn0=float(ebn0), eps=None,
+                            bits_max=1e7, n_err_min=1e5,
+                            file="ber_vs_ibo_%s_los_nant64_ebn0_%d_ibo_min0_max9_step0.50_%s" % (rx, ebn0, TAIL)))
+        for ch in ("rayleigh", "two_path"):
+            out.append(dict(family="ibo", receiver=rx, channel=ch, n_ant=64, axis="ibo", ebn0=15.0, eps=None,
+                            bits_max=1e7, n_err_min=1e5,
+                            file="ber_vs_ibo_%s_%s_nant64_ebn0_15_ibo_min0_max8_step0.50_%s" % (rx, ch, TAIL)))
+    for rx in ("cnc", "mcnc"):
+        for ch in ("los", "rayleigh", "two_path"):
+            for na in (1, 4):
+                out.append(dict(family="small", receiver=rx, channel=ch, n_ant=na, axis="ibo", ebn0=15.0, eps=None,
+                                bits_max=1e7, n_err_min=1e5,
+                                file="ber_vs_ibo_%s_%s_nant%d_ebn0_15_ibo_min0_max9_step0.50_%s" % (rx, ch, na, TAIL)))
+    return out
+
+
+CURVES = _curves()
+
+
+def curve_name(c):
+    tag = "eps%.1f" % c["eps"] if c["family"] == "csi" else "ebn0_%g" % c["ebn0"]
+    return "%s_%s_%s_nant%d_%s" % (c["family"], c["receiver"], c["channel"], c["n_ant"], tag)
+
+
+def published(c):
+    import utilities
+    rows = np.asarray(utilities.read_from_csv("published_" + c["file"], directory=GOLDEN), dtype=np.float64)
+    return rows[0], rows[1:]  # axis; counter rows x points (ROW_MAPS)
+
+
+# Published counter row -> engine column ([clean, standard RX, iterations 1..8]).  The CSI
+# files hold all ten rows the committed drivers write ("full").  The BER-vs-IBO files hold
+# nine, written by earlier driver revisions, in two layouts the data tell apart (the
+# no-distortion row is flat in IBO and 0 at Eb/N0 1000; the standard RX falls with IBO):
+# the 64-antenna LoS files are [clean, standard RX, iterations 1..7] ("prefix"); the
+# Rayleigh / two-path IBO 0..8.5 files and the 1- / 4-antenna files are [standard RX,
+# iterations 1..8] -- incl_clean_run False, as final_plots/ber_vs_ibo.py:22-40 reads them
+# ("no_clean").  measure() reports the fit of the other layouts too.
+ROW_MAPS = {"full": lambda r: list(range(r)), "prefix": lambda r: list(range(r)),
+            "no_clean": lambda r: list(range(1, r + 1)), "skip_std": lambda r: [0] + list(range(2, r + 1))}
+
+
+def layout(c):
+    if c["family"] == "csi":
+        return "full"
+    return "prefix" if c["family"] == "ibo" and c["channel"] == "los" else "no_clean"
+
+
+def points(c, axis):
+    """Per-point engine parameters, through the Link's own object state (update_distortion /
+    set_snr as the drivers call them)."""
+    from link_util import build_link
+    from utilities import ebn0_to_snr
+    link, _ = build_link(n_ant=c["n_ant"], n_sc=N_SC, n_fft=N_FFT, M=M, cp=128, ibo=0.0, chan=c["channel"],
+                         is_mcnc=c["receiver"] == "mcnc", csi=c["eps"])
+    pts = []
+    for v in axis:
+        ibo, ebn0 = (c["ibo"], v) if c["axis"] == "ebn0" else (v, c["ebn0"])
+        link.update_distortion(float(ibo))
+        link.set_snr(float(ebn0_to_snr(float(ebn0), N_SC, N_SC, M)))
+        pts.append(link.point_params())
+    return link, pts
+
+
+def stop_trials(ber, bits_max, n_err_min):
+    """Trials the reference's stopping rule gives a counter of this BER (at least one)."""
+    cap = np.ceil(bits_max / BPS)
+    with np.errstate(divide="ignore"):
+        need = np.where(ber > 0, np.ceil(n_err_min / np.maximum(ber, 1e-300) / BPS), cap)
+    return np.maximum(1.0, np.minimum(cap, need))
+
+
+def run_engine(link, pts, n_tr, seed0, precision=None):
+    import _engine
+    from channel import carrier_freqs
+    m, rx = link.my_mod, link.my_standard_rx
+    eng = _engine.Engine(link.n_ant_val, m.n_sub_carr, m.n_fft, m.constel_size, m.cp_len, link._chan_kind(),
+                         "mcnc" if link.is_mcnc else "cnc", link.my_array.positions(),
+                         (link.rx_loc_x, link.rx_loc_y, rx.cord_z), link.rx_loc_var,
+                         carrier_freqs(m.n_fft, rx.carrier_spacing, rx.center_freq), device=0, precision=precision)
+    n_pt = len(pts)
+    t0 = time.perf_counter()
+    err, bits, per = eng.run_points(pts, [seed0 + j for j in range(n_pt)], [0] * n_pt, [n_tr] * n_pt, ITERS, True,
+                                    per_trial=True)
+    dt = time.perf_counter() - t0
+    eng.close()
+    return err, bits, per.reshape(n_pt, n_tr, len(ITERS) + 1), dt
+
+
+def compare(ber, sd, q, pub, n_tr, bits_max, n_err_min, err):
+    """z statistics, bias and zero-region figures of one curve ([counter, point] arrays)."""
+    n_ref = stop_trials(ber, bits_max, n_err_min)
+    sig_gpu = sd / np.sqrt(n_tr)
+    sig_ref = sd / np.sqrt(n_ref)
+    ref_errs = pub * n_ref * BPS
+    sel = (pub >= 1e-5) & (ref_errs >= 100) & (sd > 0)
+    z = (ber - pub) / np.sqrt(sig_gpu ** 2 + sig_ref ** 2 + 1e-300)
+    rel = (ber - pub) / np.where(sel, pub, 1.0)
+    zs = np.abs(z[sel])
+    zero = pub == 0              # the reference saw no erroneous symbol in n_ref trials
+    p_zero = np.where(zero, (1.0 - q) ** n_ref, 1.0)
+    ours_zero = (err == 0) & (pub > 0)
+    rows = range(pub.shape[0])
+    # the trial count that would make the published scatter about the engine's estimate
+    # normal (mean z^2 = 1 with sigma_ref = sd / sqrt(n)): compare with the stopping rule's
+    d2, sd2, sg2 = (ber - pub)[sel] ** 2, sd[sel] ** 2, sig_gpu[sel] ** 2
+    n_eff = None
+    if zs.size:
+        lo, hi = 1.0, 1e7
+        for _ in range(100):
+            mid = np.sqrt(lo * hi)
+            lo, hi = (mid, hi) if np.mean(d2 / (sg2 + sd2 / mid)) < 1.0 else (lo, mid)
+        n_eff = round(float(np.sqrt(lo * hi)), 1)
+    out = dict(compared=int(sel.sum()), n_ref_median=float(np.median(n_ref[sel])) if zs.size else None,
+               n_eff=n_eff,
+               frac_abs_z_le1=round(float((zs <= 1).mean()), 4) if zs.size else None,
+               frac_abs_z_le2=round(float((zs <= 2).mean()), 4) if zs.size else None,
+               mean_z2=round(float((zs ** 2).mean()), 3) if zs.size else None,
+               max_abs_z=round(float(zs.max()), 3) if zs.size else None,
+               median_abs_rel=round(float(np.median(np.abs(rel[sel]))), 5) if zs.size else None,
+               row_mean_z={str(r): round(float(z[r][sel[r]].mean()), 3) for r in rows if sel[r].sum() >= 3},
+               row_mean_rel={str(r): round(float(rel[r][sel[r]].mean()), 5) for r in rows if sel[r].sum() >= 3},
+               zero_points=int(zero.sum()), min_p_zero=round(float(p_zero.min()), 6),
+               pub_pos_ours_zero=int(ours_zero.sum()),
+               pub_pos_ours_zero_max_ref_errs=round(float(ref_errs[ours_zero].max()), 2) if ours_zero.any() else 0.0)
+    return out, z, sel
+
+
+def measure(c, n_tr=None, seed0=5150, f32_check=False):
+    """The engine's estimate of every counter of every point of curve ``c`` against the
+    published one.  Returns (summary dict, arrays)."""
+    axis, pub = published(c)
+    n_pt, R = len(axis), pub.shape[0]
+    if n_tr is None:
+        n_tr = 4096 if c["receiver"] == "mcnc" and c["n_ant"] > 4 else 8192
+    link, pts = points(c, axis)
+    err, bits, per, dt = run_engine(link, pts, n_tr, seed0)
+    ber = (err / bits).T                                    # [column, point]
+    sd = (per.astype(np.float64) / BPS).std(axis=1, ddof=1).T
+    q = (per > 0).mean(axis=1).T                            # fraction of trials holding any error
+    main = layout(c)
+    maps = [main] if R == len(ITERS) + 1 else [main] + [m for m in ("prefix", "no_clean", "skip_std") if m != main]
+    out = dict(curve=curve_name(c), file=c["file"], n_tr=n_tr, points=n_pt, rows=R, layout=main,
+               seconds=round(dt, 2))
+    arrays = None
+    for name in maps:
+        cols = ROW_MAPS[name](R)
+        st, z, sel = compare(ber[cols], sd[cols], q[cols], pub, n_tr, c["bits_max"], c["n_err_min"], err.T[cols])
+        if name == main:
+            out.update(st)
+            out["z_map"] = [[round(float(v), 2) if s else None for v, s in zip(zr, sr)] for zr, sr in zip(z, sel)]
+            arrays = dict(axis=axis, ber=ber[cols], pub=pub, z=z, sel=sel)
+        else:
+            out["alt_" + name] = dict(mean_z2=st["mean_z2"], frac_abs_z_le1=st["frac_abs_z_le1"],
+                                      compared=st["compared"])
+    if f32_check:
+        e32, b32, per32, _ = run_engine(link, pts, n_tr, seed0, precision="f32")
+        out["f32_entry_agreement"] = round(float((per32 == per).mean()), 6)
+        out["f32_total_err_ratio"] = round(float(e32.sum() / max(1, err.sum())), 6)
+        cols = ROW_MAPS[main](R)
+        st32, _, _ = compare((e32 / b32).T[cols], sd[cols], q[cols], pub, n_tr, c["bits_max"], c["n_err_min"],
+                             e32.T[cols])
+        out["f32_mean_z2"], out["f32_compared"] = st32["mean_z2"], st32["compared"]
+    return out, arrays
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--family", default="all")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--n-tr", type=int, default=None)
+    a = ap.parse_args()
+    res = []
+    for c in CURVES:
+        if a.family != "all" and c["family"] != a.family:
+            continue
+        r, _ = measure(c, a.n_tr, f32_check=c.get("ebn0") == 1000.0)
+        print(json.dumps(r), flush=True)
+        res.append(r)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
