@@ -161,10 +161,10 @@ def acquire_device_slot(dev: int) -> bool:
 
 
 def slot_heartbeat(dev: int) -> None:
-    """A slot holder's sign of life: touch its lock file (once before its engine set-up and
-    once per batch), so that waiting workers see progress even while the holder's first
-    batch -- engine creation, a 65,536-trial launch of a large array -- has not yet moved
-    the shared counters."""
+    """A slot holder's sign of life: touch its lock file (``SlotHeartbeat`` does it every
+    second while ``simulate`` runs), so that waiting workers see progress even while the
+    holder's first batch -- engine creation, a 65,536-trial launch of a large array -- has
+    not yet moved the shared counters."""
     fd = _SLOTS.get((os.getpid(), int(dev)))
     if fd is not None:
         try:
@@ -173,8 +173,41 @@ def slot_heartbeat(dev: int) -> None:
             pass
 
 
+class SlotHeartbeat:
+    """Beats this process's slot heartbeat every ``period_s`` (MIMO_SLOT_HEARTBEAT_S, default
+    1 s) from a daemon thread while the block runs, so that one long launch -- the engine
+    call releases the GIL -- still reads as progress to waiting workers (beats
+    only before set-up and after each batch let a first batch longer than the stall time
+    trigger the waiters' escape)."""
+
+    def __init__(self, dev: int, period_s: float = None):
+        import threading
+        self.dev = int(dev)
+        self.period_s = float(os.environ.get("MIMO_SLOT_HEARTBEAT_S", "1.0")) if period_s is None else period_s
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self._stop.wait(self.period_s):
+            slot_heartbeat(self.dev)
+
+    def __enter__(self):
+        slot_heartbeat(self.dev)
+        self._thread.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._thread.join()
+        return False
+
+
 def slot_activity(dev: int) -> int:
-    """Latest heartbeat (lock-file mtime, ns) of ``dev``'s slots; 0 if none."""
+    """Latest heartbeat (lock-file mtime, ns) of ``dev``'s slots; 0 if none.  Any holder's
+    beat counts, including a holder busy with other counters (another grid point, another
+    driver sharing the lock directory): a waiter then keeps waiting until such holders
+    finish their runs instead of creating an extra engine -- bounded by those runs, never a
+    deadlock, since a holder's slot is released when its process exits."""
     d = _slot_dir()
     cap = max(1, int(os.environ.get("MIMO_MAX_ENGINES_PER_DEVICE", "2")))
     latest = 0
@@ -344,7 +377,12 @@ class Link:
                 return
         else:
             acquire_device_slot(dev)  # private counters: nobody else closes them, never wait
-        slot_heartbeat(dev)
+        with SlotHeartbeat(dev):
+            self._simulate_loop(incl_clean_run, reroll_chan, cnc_n_iter_lst, seed_arr, n_err_shared_arr,
+                                n_bits_sent_shared_arr, err_np)
+
+    def _simulate_loop(self, incl_clean_run, reroll_chan, cnc_n_iter_lst, seed_arr, n_err_shared_arr,
+                       n_bits_sent_shared_arr, err_np):
         eng = self.engine(reroll_chan)
         seed = _seed64(seed_arr)
         iters_all = np.asarray(cnc_n_iter_lst, dtype=np.int64).reshape(-1)
@@ -367,7 +405,6 @@ class Link:
                            self.max_batch)
             uniq = sorted(set(run_iters))
             e, b, _ = eng.run(seed, trial, n, uniq, clean_on)
-            slot_heartbeat(dev)
             trial += n
             pos = {it: j + (1 if clean_on else 0) for j, it in enumerate(uniq)}
             lock = n_err_shared_arr.get_lock() if hasattr(n_err_shared_arr, "get_lock") else None

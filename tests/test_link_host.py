@@ -244,6 +244,11 @@ def _slow_holder(lock_dir, beat, hold_s, q):
     os.environ["MIMO_MAX_ENGINES_PER_DEVICE"] = "1"
     import mp_model
     q.put(mp_model.acquire_device_slot(0))
+    if beat == "thread":
+        # one long blocking call (a launch, GIL released) inside simulate()'s heartbeat thread
+        with mp_model.SlotHeartbeat(0, period_s=0.2):
+            time.sleep(hold_s)
+        return
     t0 = time.monotonic()
     while time.monotonic() - t0 < hold_s:
         if beat:
@@ -251,7 +256,7 @@ def _slow_holder(lock_dir, beat, hold_s, q):
         time.sleep(0.2)
 
 
-@pytest.mark.parametrize("beat", [True, False])
+@pytest.mark.parametrize("beat", [True, False, "thread"])
 def test_slot_wait_counts_holder_heartbeats_as_progress(tmp_path, monkeypatch, beat):
     """a holder whose first batch outlasts the stall time still counts as working
     when it beats its slot's heartbeat: the waiter keeps waiting (no extra engine) and takes
