@@ -93,28 +93,53 @@ def owned_points(n_points: int, rank: int, world: int, costs=None) -> list:
     return sorted(mine)
 
 
+# Residual clipping distortion seen by a point's best counter, relative to the soft
+# limiter's signal-to-distortion ratio at the point's IBO (point_costs): with MRT over
+# i.i.d. Rayleigh the distortion is not beamformed (~1/A of it reaches the user); over LoS /
+# two-path it is, and the CNC / MCNC iterations remove ~90 % of it.  Calibrated on the
+# committed one-GPU records of the 915-point grid (profiles/r05/grid/, tests/test_grid_balance.py).
+RESIDUAL_DISTORTION = {"rayleigh": None, "los": 0.1, "two_path": 0.1}
+
+
+def soft_limiter_sdr(ibo_db):
+    """Bussgang signal-to-distortion ratio of the soft limiter for a complex Gaussian input
+    at IBO ``ibo_db``: alpha^2 / (E|y|^2 / P - alpha^2), E|y|^2 / P = 1 - exp(-gamma^2),
+    alpha = calc_alpha (modulation.py:178-189)."""
+    from scipy import special
+    g2 = 10 ** (np.asarray(ibo_db, dtype=np.float64) / 10)
+    g = np.sqrt(g2)
+    a = 1 - np.exp(-g2) + np.sqrt(np.pi) / 2 * g * special.erfc(g)
+    return a ** 2 / np.maximum(1 - np.exp(-g2) - a ** 2, 1e-300)
+
+
 def point_costs(ibo_arr, ebn0_arr, n_bits_per_sym, constel_size, n_err_min, bits_sent_max, iters, n_ant=64,
-                is_mcnc=False):
+                is_mcnc=False, channel="rayleigh", pilot=64):
     """Relative cost of every (IBO, Eb/N0) point for sharding: expected trials x cost per trial.
 
     Trials: a point runs until its best counter has n_err_min errors or the bit budget is
-    spent (mp_model.py:177-187); the best counter's BER is estimated by Gray-QAM over AWGN
-    at the point's Eb/N0 (a lower bound: clipping only adds errors), so low-SNR points are
-    cheap and high-SNR points hit bits_sent_max.  Per trial: one array pass (n_ant FFT pairs)
-    plus one FFT pair per CNC iteration, or one more array pass per MCNC iteration."""
+    spent (mp_model.py:177-187), and at least the stopping rule's pilot batch
+    (mp_model.PILOT).  The best counter's BER is Gray-QAM at the SINR that the noise and the
+    residual clipping distortion leave, 1 / (1 / snr + kappa / sdr(IBO)) with kappa from
+    RESIDUAL_DISTORTION (1/A for Rayleigh), so low-SNR points and low-IBO LoS points are
+    cheap and the rest hit bits_sent_max.  Per trial: one array pass (n_ant FFT pairs) plus
+    one FFT pair per CNC iteration, or one more array pass per MCNC iteration."""
     from scipy import special
     M = float(constel_size)
     k = np.log2(M)
     budget = bits_sent_max / n_bits_per_sym
     max_it = int(np.max(iters)) if len(iters) else 0
     per_trial = n_ant * (1 + max_it) if is_mcnc else n_ant + max_it
+    kappa = RESIDUAL_DISTORTION.get(channel, 0.1)
+    kappa = 1.0 / max(1, n_ant) if kappa is None else kappa
+    sdr = soft_limiter_sdr(np.asarray(ibo_arr, dtype=np.float64))
     out = np.zeros(len(ibo_arr) * len(ebn0_arr))
     for i in range(len(ibo_arr)):
         for j, e in enumerate(ebn0_arr):
-            g = 10 ** (e / 10)
-            ber = 2 / k * (1 - 1 / np.sqrt(M)) * special.erfc(np.sqrt(1.5 * k * g / (M - 1)))
+            snr = 10 ** (e / 10) * k  # Es/N0 per symbol
+            sinr = 1.0 / (1.0 / snr + kappa / sdr[i])
+            ber = 2 / k * (1 - 1 / np.sqrt(M)) * special.erfc(np.sqrt(1.5 * sinr / (M - 1)))
             trials = min(budget, n_err_min / max(ber * n_bits_per_sym, 1e-30))
-            out[i * len(ebn0_arr) + j] = max(trials, 1.0) * per_trial
+            out[i * len(ebn0_arr) + j] = max(trials, float(pilot), 1.0) * per_trial
     return out
 
 
@@ -139,9 +164,10 @@ def run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean=True, seed=2137, rank=0,
     counts = np.zeros((n_pts, n_idx, 2), dtype=np.int64)
     m = link.my_mod
     n_bits_sym = int(m.n_sub_carr * np.log2(m.constel_size))
+    chan = link._chan_kind() if hasattr(link, "_chan_kind") else "rayleigh"
     costs = point_costs(ibo_arr, ebn0_arr, n_bits_sym, m.constel_size, getattr(link, "n_err_min", 1e5),
                         getattr(link, "bits_sent_max", 5e6), iters, getattr(link, "n_ant_val", 64),
-                        getattr(link, "is_mcnc", False))
+                        getattr(link, "is_mcnc", False), chan)
     mine = owned_points(n_pts, rank, world, costs)
     t_start = time.perf_counter()
     sim_stats = {}
