@@ -52,6 +52,8 @@ WORKLOADS = {
                   desc="config 2 with the MCNC receiver (one full array pass per iteration)"),
     "2csi": dict(A=64, S=1024, F=2048, M=64, CP=128, pa="softlim", p=0.0, ibo=3.0, ebn0=15.0, csi=0.1,
                  desc="config 2 with imperfect CSI (epsilon 0.1, mp_model.py:253-288)"),
+    "papercsi": dict(A=64, S=2048, F=4096, M=64, CP=128, pa="softlim", p=0.0, ibo=3.0, ebn0=15.0, csi=0.1,
+                     desc="paper config with imperfect CSI (epsilon 0.1, mp_model.py:253-288)"),
     "5su": dict(A=256, S=4096, F=8192, M=64, CP=128, pa="rapp", p=3.0, ibo=3.0, ebn0=15.0,
                 desc="config-5 array at one user: 256-ant MRT, 4096-sc (FFT 8192) 64-QAM, Rapp p=3 IBO 3 dB, "
                      "Rayleigh, Eb/N0 15 dB"),

@@ -399,7 +399,25 @@ int ensure_device(mimo_engine* e) {
     }
     return tw;
   };
-  auto twiddles = [&](int T, auto cvt) { return twiddles_of(F, T, cvt); };
+  // cot-tan constants of the twiddled stages (team_fft.h dft8_ct / dft16_ct), appended to a
+  // stage table: (cos a, tan a) per (stage, row, lane); cos is never exactly 0 in double
+  // (cos(pi/2) = 6.1e-17), so tan stays finite
+  auto append_ct = [](auto& tw, int Fs, int P, auto cvt) {
+    for (int st = 1; st < mimo::fft_nst(Fs, P); ++st) {
+      const int NS = 1 << mimo::fft_bits_before(Fs, P, st), R = 1 << mimo::fft_bits(Fs, P, st);
+      for (int q = 0; q < mimo::ct_rows(R); ++q)
+        for (int jm = 0; jm < NS; ++jm) {
+          const double a = 2.0 * M_PI * mimo::ct_rev(R, NS, jm, q), c = std::cos(a);
+          tw.push_back(cvt(c, std::sin(a) / c));
+        }
+    }
+  };
+  auto twiddles = [&](int T, auto cvt) {
+    auto tw = twiddles_of(F, T, cvt);
+    tw.resize(std::max(1, mimo::fft_tw_total(F, F / T)));
+    if (F / T >= 2) append_ct(tw, F, F / T, cvt);
+    return tw;
+  };
   auto to_f32 = [](double c, double s) { return make_float2((float)c, (float)s); };
   auto to_f64 = [](double c, double s) { return make_double2(c, s); };
   std::vector<float2> tws[2] = {twiddles(mimo::team_size(F), to_f32), twiddles(mimo::alt_team_size(F), to_f32)};
@@ -412,6 +430,7 @@ int ensure_device(mimo_engine* e) {
       const double ang = -2.0 * M_PI * (double)n / (double)F;
       tw.push_back(cvt(std::cos(ang), std::sin(ang)));
     }
+    append_ct(tw, mimo::wave_fft_fw(F, T), F / T, cvt);  // the sub-transforms' cot-tan region
     return tw;
   };
   std::vector<double2> twave64;

@@ -276,6 +276,94 @@ struct Dft {
   };
 };
 
+// ---------------------------------------------------------------- twiddles absorbed into FMAs
+// A twiddle z = c + j s stored as (c, t = s / c) ("cot-tan" form): z b = c (b + j t b), so a
+// radix-2 butterfly a +- z b is u = (b.x - t b.y, b.y + t b.x) and a +- c u -- 6 FMAs instead
+// of a complex multiply (2 mul + 2 fma) and 4 additions.  The inverse uses conj(z): t -> -t.
+// ROT: the twiddle times rho = DIR j (W_4 of the transform's direction) -- operands swapped,
+// still 6 FMAs.  Exact in the limit c -> 0 as long as c != 0 (the host tables hold
+// cos(pi/2) = 6.1e-17, never 0): c t rounds to s, and the dropped b term is c b ~ 1e-16 b.
+template <int DIR, bool ROT, class C, typename Re = real_of<C>>
+__device__ __forceinline__ void bfly_ct(C a, C b, C ct, C& o0, C& o1) {
+  const Re c = ct.x, tt = DIR < 0 ? ct.y : -ct.y;
+  const Re ux = fmar(-tt, b.y, b.x), uy = fmar(tt, b.x, b.y);
+  if constexpr (!ROT) {
+    o0 = mkc(fmar(c, ux, a.x), fmar(c, uy, a.y));
+    o1 = mkc(fmar(-c, ux, a.x), fmar(-c, uy, a.y));
+  } else {
+    const Re cd = DIR < 0 ? -c : c;  // rho c u = cd (-u.y, u.x)
+    o0 = mkc(fmar(-cd, uy, a.x), fmar(cd, ux, a.y));
+    o1 = mkc(fmar(cd, uy, a.x), fmar(-cd, ux, a.y));
+  }
+}
+// y[k] = sum_r W8^(r k) z^r v[r] (natural order in and out) as three radix-2 DIT levels with
+// every twiddle absorbed (12 butterflies = 72 FMAs, against 7 complex multiplies + the
+// 52-op DFT-8 = 80): level 1 pairs (r, r + 4) with z^4, level 2 (r0, r0 + 2) with
+// W4^k0 z^2, level 3 (0, 1) with W8^m z.  zc: (c, t) of z^4, z^2, z and W8 z (forward W8 =
+// e^{-j pi / 4}; the inverse conjugates all of them).
+template <int DIR, class C>
+__device__ __forceinline__ void dft8_ct(C (&v)[8], const C (&zc)[4]) {
+  C a0[4], a1[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bfly_ct<DIR, false>(v[r], v[r + 4], zc[0], a0[r], a1[r]);
+  C b[2][4];
+#pragma unroll
+  for (int r0 = 0; r0 < 2; ++r0) {
+    bfly_ct<DIR, false>(a0[r0], a0[r0 + 2], zc[1], b[r0][0], b[r0][2]);
+    bfly_ct<DIR, true>(a1[r0], a1[r0 + 2], zc[1], b[r0][1], b[r0][3]);
+  }
+  bfly_ct<DIR, false>(b[0][0], b[1][0], zc[2], v[0], v[4]);
+  bfly_ct<DIR, false>(b[0][1], b[1][1], zc[3], v[1], v[5]);
+  bfly_ct<DIR, true>(b[0][2], b[1][2], zc[2], v[2], v[6]);
+  bfly_ct<DIR, true>(b[0][3], b[1][3], zc[3], v[3], v[7]);
+}
+// The same for R = 16 (four levels, 32 butterflies = 192 FMAs, against 15 complex
+// multiplies, the products forming 11 of the 15 twiddles and the ~152-op DFT-16): level 1
+// (r, r + 8) with z^8, level 2 (r, r + 4) with W4^k0 z^4, level 3 (r0, r0 + 2) with W8^m z^2,
+// level 4 (0, 1) with W16^m z.  zc: (c, t) of z^8, z^4, z^2, W8 z^2, z, W16 z, W8 z, W16^3 z.
+template <int DIR, class C>
+__device__ __forceinline__ void dft16_ct(C (&v)[16], const C (&zc)[8]) {
+  C a[2][8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) bfly_ct<DIR, false>(v[r], v[r + 8], zc[0], a[0][r], a[1][r]);
+  C b[4][4];  // b[r][m], m = k mod 4
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    bfly_ct<DIR, false>(a[0][r], a[0][r + 4], zc[1], b[r][0], b[r][2]);
+    bfly_ct<DIR, true>(a[1][r], a[1][r + 4], zc[1], b[r][1], b[r][3]);
+  }
+  C c[2][8];  // c[r0][m], m = k mod 8
+#pragma unroll
+  for (int r0 = 0; r0 < 2; ++r0) {
+    bfly_ct<DIR, false>(b[r0][0], b[r0 + 2][0], zc[2], c[r0][0], c[r0][4]);
+    bfly_ct<DIR, false>(b[r0][1], b[r0 + 2][1], zc[3], c[r0][1], c[r0][5]);
+    bfly_ct<DIR, true>(b[r0][2], b[r0 + 2][2], zc[2], c[r0][2], c[r0][6]);
+    bfly_ct<DIR, true>(b[r0][3], b[r0 + 2][3], zc[3], c[r0][3], c[r0][7]);
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    bfly_ct<DIR, false>(c[0][m], c[1][m], zc[4 + m], v[m], v[m + 8]);
+    bfly_ct<DIR, true>(c[0][m + 4], c[1][m + 4], zc[4 + m], v[m + 4], v[m + 12]);
+  }
+}
+// Host / device: the cot-tan rows of a radix-R stage (R = 8: 4 rows, 16: 8 rows), lane jm,
+// z = exp(-j 2 pi jm / (R NS)), as angles in revolutions (ct_rows, ct_rev).
+__host__ __device__ constexpr int ct_rows(int R) { return R == 8 ? 4 : 8; }
+__host__ __device__ constexpr double ct_rev(int R, int ns, int jm, int q) {
+  const double th = -(double)jm / ((double)R * ns);
+  if (R == 8) return q == 0 ? 4 * th : q == 1 ? 2 * th : q == 2 ? th : th - 0.125;
+  switch (q) {
+    case 0: return 8 * th;
+    case 1: return 4 * th;
+    case 2: return 2 * th;
+    case 3: return 2 * th - 0.125;
+    case 4: return th;
+    case 5: return th - 0.0625;
+    case 6: return th - 0.125;
+    default: return th - 0.1875;
+  }
+}
+
 // Exchange synchronisation: the whole team (s_barrier) or, for a one-wave transform
 // (WAVE, wave_fft.h), the wave alone.  A wave's LDS instructions execute in issue order,
 // so its own exchanges need only a compiler-level fence, no hardware barrier.
@@ -294,7 +382,8 @@ __device__ __forceinline__ void xchg_sync() {
 // LTW1: stage 1's twiddle block comes from an LDS copy (run()'s tw1 argument; the wave-split
 // FFT's one-wave sub-transforms, whose stage-1 block is small: 64 entries at F 2048) -- all
 // R - 1 twiddles read, none formed as products (fp64: 16 VALU ops per stage saved).
-template <int F, int T, int NBUF = 2, typename Re = float, bool WAVE = false, bool LTW1 = false, bool LTW2_ON = false>
+template <int F, int T, int NBUF = 2, typename Re = float, bool WAVE = false, bool LTW1 = false, bool LTW2_ON = false,
+          bool CT_ON = false>
 struct TeamFft {
   using C = cx<Re>;
   static constexpr int P = F / T;
@@ -344,10 +433,29 @@ struct TeamFft {
   // fp64 F 2048 team's 3-teams-per-CU LDS line.)
   static constexpr bool LTW2 = LTW1 && LTW2_ON && NST >= 3 && fft_bits(F, P, 2) == 3;
   static constexpr int NS2 = NST >= 3 ? 1 << fft_bits_before(F, P, 2) : 1;
-  static constexpr int TWL_N = TW1_N + (LTW2 ? 3 * NS2 : 0);  // entries of the LDS copy
-  // source index in the twiddle table of LDS-copy entry i < TWL_N
+  // CT (fp64, every stage >= 1 radix 8, both stages' constants in the LDS copy): the
+  // twiddled stages run dft8_ct on cot-tan constants, [4][NS] per stage (ct_off), which
+  // replace stage 1's block and stage 2's rows in the LDS copy.
+  // CT (fp64): every twiddled stage (radix 8 or 16) runs dft8_ct / dft16_ct on cot-tan
+  // constants, [ct_rows][NS] per stage at ct_off(s) of the cot-tan region: in the LDS copy
+  // for the wave-local sub-transforms (which then replace stage 1's block and stage 2's
+  // rows; both stages must fit), else read from global memory after the stage twiddle table
+  // (fft_tw_total).  A thread's butterflies share one twiddle set (NS <= T, tw_shift's OFF = 0).
+  static constexpr bool ct_ok() {
+    for (int s = 1; s < NST; ++s)
+      if (fft_bits(F, P, s) != 3 && fft_bits(F, P, s) != 4) return false;
+    return NST >= 2;
+  }
+  static constexpr bool CT = CT_ON && sizeof(Re) == 8 && ct_ok() && (!WAVE || (LTW1 && LTW2 && NST == 3));
+  static constexpr int ct_off(int s) {
+    return s <= 1 ? 0 : ct_off(s - 1) + ct_rows(1 << fft_bits(F, P, s - 1)) * (1 << fft_bits_before(F, P, s - 1));
+  }
+  static constexpr int CT_N = CT ? ct_off(NST) : 0;  // cot-tan entries
+  static constexpr int TWL_N = CT && WAVE ? CT_N : TW1_N + (LTW2 ? 3 * NS2 : 0);  // entries of the LDS copy
+  // source index in the twiddle table of LDS-copy entry i < TWL_N (CT: relative to the
+  // cot-tan region, which the caller's table places)
   static __host__ __device__ constexpr int twl_src(int i) {
-    if (i < TW1_N) return i;
+    if ((CT && WAVE) || i < TW1_N) return i;
     const int j = i - TW1_N, row = j / NS2, r = row == 0 ? 3 : row == 1 ? 5 : 6;
     return fft_tw_off(F, P, 2) + r * NS2 + j % NS2;
   }
@@ -392,7 +500,15 @@ struct TeamFft {
     for (int r = 0; r < R; ++r) v[r] = d[I + r * B];
     const int j = t + T * I;
     const int jm = j & (NS - 1);
-    if constexpr (NS > 1) {
+    if constexpr (CT && S >= 1) {
+      if constexpr (R == 8) {
+        const C zc[4] = {w0[0], w0[1], w0[2], w0[3]};
+        dft8_ct<DIR>(v, zc);
+      } else {
+        const C zc[8] = {w0[0], w0[1], w0[2], w0[3], w0[4], w0[5], w0[6], w0[7]};
+        dft16_ct<DIR>(v, zc);
+      }
+    } else if constexpr (NS > 1) {
       constexpr int OFF = (T * I) & (NS - 1);
       C w[R];
       if constexpr (OFF == 0) {
@@ -404,7 +520,7 @@ struct TeamFft {
 #pragma unroll
       for (int r = 1; r < R; ++r) v[r] = DIR < 0 ? cmul(v[r], w[r]) : cmulc(v[r], w[r]);
     }
-    Dft<R, DIR, (S == 0 ? bfly_mask(ZM, I, B, R) : 0u)>::run(v);
+    if constexpr (!(CT && S >= 1)) Dft<R, DIR, (S == 0 ? bfly_mask(ZM, I, B, R) : 0u)>::run(v);
     if constexpr (LAST) {
 #pragma unroll
       for (int r = 0; r < R; ++r) d[I + r * B] = v[r];
@@ -471,7 +587,7 @@ struct TeamFft {
     if constexpr (S < NST) {
       constexpr int R = 1 << bits(S);
       constexpr int NS = 1 << bits_before(S);
-      if constexpr (NS > 1 && !(LTW1 && S == 1)) {
+      if constexpr (NS > 1 && !(LTW1 && S == 1) && !CT) {
         constexpr int TW_OFF = fft_tw_off(F, P, S);
         const int jm0 = t & (NS - 1);
 #pragma unroll
@@ -494,7 +610,21 @@ struct TeamFft {
     static_assert(B >= 1 && B * R == P, "radix must divide points per thread");
     C* buf = lds + (NBUF == 2 ? ((S + PAR) & 1) * LDS_ELEMS : 0);
     C w0[R];
-    if constexpr (NS > 1 && LTW1 && S == 1) {
+    if constexpr (CT && S >= 1) {
+      // cot-tan constants in w0[0 .. ct_rows) (butterfly() runs dft8_ct / dft16_ct)
+      static_assert(((T * (B - 1)) & (NS - 1)) == 0, "cot-tan stages: one twiddle set per thread");
+      constexpr int Q = ct_rows(R);
+      if constexpr (WAVE) {
+        const C* cts = tw1 + ct_off(S) + (t & (NS - 1));
+#pragma unroll
+        for (int q = 0; q < Q; ++q) w0[q] = cts[q * NS];
+      } else {
+        const C* cts = tw + fft_tw_total(F, P) + ct_off(S);
+        const int jm0 = t & (NS - 1);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) w0[q] = gload(cts + q * NS, jm0);
+      }
+    } else if constexpr (NS > 1 && LTW1 && S == 1) {
       const C* tws = tw1 + (t & (NS - 1));
 #pragma unroll
       for (int r = 1; r < R; ++r) w0[r] = tws[r * NS];

@@ -53,8 +53,10 @@ constexpr Profile profile_for(int T, bool aligned, int ch) {
 template <int T, int NSLOT, bool AL, int CH, bool CSI>
 hipError_t go(dim3 grid, hipStream_t st, const TrialParams<Real>& p) {
   constexpr Profile pr = profile_for(T, AL, CH);
-  hipLaunchKernelGGL((trial_kernel<Real, kF, T, NSLOT, AL, CH, CSI, pr.minw, pr.nbuf, pr.symw_lds>), grid, dim3(T), 0,
-                     st, p);
+  // CSI: the per-antenna power table is dynamic LDS, A reals (trial_kernel pw_csi)
+  const size_t dyn = CSI ? sizeof(Real) * (size_t)p.n_ant : 0;
+  hipLaunchKernelGGL((trial_kernel<Real, kF, T, NSLOT, AL, CH, CSI, pr.minw, pr.nbuf, pr.symw_lds>), grid, dim3(T),
+                     dyn, st, p);
   return hipGetLastError();
 }
 

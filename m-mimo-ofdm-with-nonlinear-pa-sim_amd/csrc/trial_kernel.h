@@ -41,7 +41,7 @@ enum PaKind : int { PA_NONE = 0, PA_SOFTLIM = 1, PA_RAPP = 2, PA_TOI = 3 };
 enum ChanKind : int { CH_RAYLEIGH = 1, CH_LOS = 2, CH_TWOPATH = 3, CH_TABLE = 4 };
 enum RxKind : int { RX_CNC = 1, RX_MCNC = 2 };
 
-constexpr int kMaxCsiAnt = 512;  // CSI-error runs: antennas (LDS per team; engine.hip checks)
+constexpr int kMaxCsiAnt = 512;  // CSI-error runs: antennas (dynamic LDS per team, A doubles; engine.hip checks)
 constexpr uint32_t kFixedCsiTrial = 0xFFFFFFFFu;  // CSI stream counter of fixed-channel runs (oracle/sim.py draws)
 // The measured alternatives of the choices below (channel pipeline on / off per precision,
 // register diet from F 8192, raw-word pipeline, alpha by library exp / erfc, shfl vs DPP
@@ -104,8 +104,16 @@ struct TrialParams {
 // Ablation switches for cost breakdowns.  Compiled in only with -DMIMO_ABLATION
 // (libmimo_engine_ablation.so); the production kernel has none of these branches.
 enum : uint32_t { ABL_RNG = 1, ABL_FFT = 2, ABL_PASS1 = 4, ABL_PA = 8, ABL_XCHG = 16 };
+// ISA inspection only (tools/stage_hist.py): a comment in the assembly naming the loop.
+#ifdef MIMO_ISA_MARKERS
+#define MIMO_ISA_MARK(name) asm volatile("; MIMO_MARK " name)
+#else
+#define MIMO_ISA_MARK(name) ((void)0)
+#endif
 #ifdef MIMO_ABLATION
 #define MIMO_ABL(p, bit) (((p).ablate & (bit)) != 0)
+#elif defined(MIMO_STATIC_ABLATE)  // ISA inspection only (tools/stage_hist.py): stages compiled out
+#define MIMO_ABL(p, bit) ((MIMO_STATIC_ABLATE & (bit)) != 0)
 #else
 #define MIMO_ABL(p, bit) false
 #endif
@@ -668,12 +676,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   using CParams = const __attribute__((address_space(4))) TrialParams<R>;
   CParams& p = *(CParams*)(p0.points + pi);
   constexpr bool WAVEFFT = wave_fft_used(F, T, sizeof(R) == 8);
-  // CSI instances read only stage 1's twiddle block from LDS, not stage 2's rows: with
-  // their 4 KiB per-antenna power table the 3 KiB of rows would cross the 3-teams-per-CU
-  // line (LDS is allocated in 512-B granules; 2 teams per CU measured +10 %).  Before the
-  // transposed exchange 0 freed 2 KiB of the wave rows the stage-1 block did not fit
-  // either; with it: -0.7 % (profiles/r04/csi/).
-  using FFT = std::conditional_t<WAVEFFT, WaveFft<F, T, R, true, !CSI>, TeamFft<F, T, NBUF, R>>;
+  // The sub-transforms read their twiddled stages' constants from LDS (stage 1's block and
+  // stage 2's rows; fp64: the cot-tan constants of dft8_ct).  CSI instances too, since their
+  // per-antenna power table is dynamic LDS sized by A (round 5; before, a static 4 KiB
+  // table left no room for stage 2's rows at 3 teams per CU).
+  // fp64: the twiddled stages absorb their twiddles into FMAs (team_fft.h dft8_ct / dft16_ct)
+  using FFT = std::conditional_t<WAVEFFT, WaveFft<F, T, R, true, true>,
+                                 TeamFft<F, T, NBUF, R, false, false, false, sizeof(R) == 8>>;
   using SL = Slots<F, T, NSLOT, ALIGNED>;
   using CHN = Channel<R, F, T, NSLOT, ALIGNED, CH>;
   constexpr int P = FFT::P;
@@ -688,7 +697,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   __shared__ C lds[FFT::LDS_TOTAL];
   __shared__ R red[T / 64];  // sized by the team
   __shared__ R vk_part[2][T / 64];
-  __shared__ R pw_csi[CSI ? kMaxCsiAnt : 1];  // per-antenna mean |H|^2 (CSI model)
+  // per-antenna mean |H|^2 (CSI model): dynamic LDS of A doubles (the launch sizes it), not
+  // a static kMaxCsiAnt table -- the static 4 KiB cost F 4096 its second team per CU and F
+  // 2048 its stage-2 twiddle rows (and with them the cot-tan FFT stages)
+  extern __shared__ __align__(16) unsigned char dyn_lds[];
+  R* pw_csi = reinterpret_cast<R*>(dyn_lds);
   __shared__ C symw_s[SYMW_LDS ? NSLOT * T : 1];  // [slot][thread]
   // wave-split FFT: the one-wave sub-transforms read stage 1's twiddles and (without CSI)
   // stage 2's rows r = 3, 5, 6 from LDS (team_fft.h TWL_N; -24 f64 ops per antenna at config 2)
@@ -769,9 +782,20 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 
   // ---- pass 1: MRT norms over the (estimated) channel
   R nrm2[NSLOT];
+  // CSI: the clean-run combine sum_a H conj(Hhat) / ||Hhat|| (mp_model.py:159-175 with the
+  // estimate's precoder) is accumulated here, where H and Hhat are both at hand, and scaled
+  // by 1 / ||Hhat|| once pass 1 has the norms -- not in the array pass, where its 16
+  // accumulator VGPRs lived across both FFTs (the CSI instance spilled 53 KB per trial of
+  // scratch writes, profiles/r05/pmc/pmc_traffic_2csi.json).
+  C cc[CSI ? NSLOT : 1];
 #pragma unroll
-  for (int s = 0; s < NSLOT; ++s) nrm2[s] = R(0);
+  for (int s = 0; s < NSLOT; ++s) {
+    nrm2[s] = R(0);
+    if constexpr (CSI) cc[s] = czero<R>();
+  }
+  const bool clean_cc = CSI && p.incl_clean;
   for (int a = 0; a < (MIMO_ABL(p, ABL_PASS1) ? 1 : A); ++a) {
+    MIMO_ISA_MARK("pass1");
     const int tl = opaque(t);
     if constexpr (CH == CH_RAYLEIGH && !CSI) {
       if (!MIMO_ABL(p, ABL_RNG)) {
@@ -805,9 +829,18 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       C zc[NSLOT];
       CHN::normals(csi_key, csi_trial, ST_CSI, (uint32_t)a, tl, S, zc);
       const R sc = p.csi_b * sqrt_ieee(pw);
+      if (clean_cc) {
 #pragma unroll
-      for (int s = 0; s < NSLOT; ++s)
-        h[s] = mkc(fmar(p.csi_a, h[s].x, sc * zc[s].x), fmar(p.csi_a, h[s].y, sc * zc[s].y));
+        for (int s = 0; s < NSLOT; ++s) {
+          const C e = mkc(fmar(p.csi_a, h[s].x, sc * zc[s].x), fmar(p.csi_a, h[s].y, sc * zc[s].y));
+          cc[s] = cadd(cc[s], cmulc(h[s], e));
+          h[s] = e;
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < NSLOT; ++s)
+          h[s] = mkc(fmar(p.csi_a, h[s].x, sc * zc[s].x), fmar(p.csi_a, h[s].y, sc * zc[s].y));
+      }
     }
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) nrm2[s] = fmar(h[s].x, h[s].x, fmar(h[s].y, h[s].y, nrm2[s]));
@@ -818,6 +851,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   for (int s = 0; s < NSLOT; ++s) {
     const bool v = (valid_mask >> s) & 1u;
     inv_nrm[s] = v ? rsq_r(nrm2[s]) : R(0);
+    if constexpr (CSI) cc[s] = cscale(cc[s], inv_nrm[s]);
     const R fr = frel_of(s);
     etac_p += v ? nrm2[s] * (fr * fr) : R(0);
   }
@@ -826,12 +860,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   C d[P];
   C r[NSLOT];
   R g[NSLOT];
-  C cc[CSI ? NSLOT : 1];  // clean-run combine sum_a H conj(Hhat)/||Hhat|| (CSI only)
 #pragma unroll
   for (int s = 0; s < NSLOT; ++s) {
     r[s] = czero<R>();
     g[s] = R(0);
-    if constexpr (CSI) cc[s] = czero<R>();
   }
 
   // ---- array pass: precode -> IFFT -> PA -> FFT -> combine, one antenna at a time.
@@ -854,7 +886,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // +1.6 % (r03 ab_s); both with the segment table +0.8 % (profiles/r04/alpha/), so it
   // keeps the library forms inline.
   constexpr bool COLD_OUT = sizeof(R) == 8 && F != 4096;
-  constexpr bool E2_RE = sizeof(R) == 8 && !SYMW_LDS;    // off: +2.8 % at F 8192 (ab_diet_prefetch.json)
+  // |Hhat|^2 for g recomputed after the FFT from the channel (fp64; off: +2.8 % at F 8192,
+  // ab_diet_prefetch.json) -- except with CSI, where that would keep the 16-VGPR estimate
+  // live across both FFTs next to the true channel: 8 VGPRs of |Hhat|^2 instead.
+  constexpr bool E2_RE = sizeof(R) == 8 && !SYMW_LDS && !CSI;
   C symw_r[SYMW_LDS || SYMW_RE ? 1 : NSLOT];
   // F 8192 (one team per CU, 256 VGPRs): the lattice levels live in LDS ([slot][thread],
   // thread-private: no barrier), not in 8 VGPRs that the allocator reloaded from scratch
@@ -928,6 +963,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       else CHN::normals(key, ch_trial, ST_CHAN, 0u, t, S, hnext, bm_c<R>(sa * sa));
     }
     for (int a = 0; a < A; ++a) {
+      MIMO_ISA_MARK("array_pass");
       const int tl = opaque(t);
       C h[NSLOT];
       if constexpr (PIPE) {
@@ -985,6 +1021,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
           const C ew = cscale(e, in * inv_sqrt_f);
           x[s] = cmulc(slab_point(s), ew);
           vk = fmar(ew.x, ew.x, fmar(ew.y, ew.y, vk));
+          if constexpr (!E2_RE) e2[s] = fmar(e.x, e.x, e.y * e.y);
         } else {
           x[s] = cmulc(symw(s), e);  // s conj(Hhat) / ||Hhat|| / sqrt(F); 0 off band (symw = 0)
           e2[s] = fmar(e.x, e.x, e.y * e.y);
@@ -1054,8 +1091,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
           } else {
             g[s] = fmar(alpha_a, e2[s], g[s]);  // sum_a alpha_a |Hhat|^2; x 1/||Hhat|| after the pass
           }
-          const C e = hest(s);
-          if constexpr (CSI) cc[s] = cadd(cc[s], cscale(cmulc(h[s], e), inv_nrm[s]));
         } else {
           acc[s] = cmac(acc[s], hest(s), y);
         }

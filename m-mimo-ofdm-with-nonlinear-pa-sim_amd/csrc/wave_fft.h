@@ -50,6 +50,14 @@ constexpr bool wave_fft_used(int F, int T, bool f64) {
 constexpr int wave_fft_fw(int F, int T) { return F / (T / 64); }
 constexpr int wave_fft_tw_inter(int F, int T) { return fft_tw_total(wave_fft_fw(F, T), F / T); }
 constexpr int wave_fft_tw_total(int F, int T) { return wave_fft_tw_inter(F, T) + F; }
+// The fp64 sub-transforms' cot-tan constants (team_fft.h dft8_ct) follow the inter twiddles:
+// stage s >= 1: [ct_rows][NS_s] entries (c, tan) (ct_rev).  Their count:
+constexpr int fft_ct_n(int F, int P) {
+  int n = 0;
+  for (int s = 1; s < fft_nst(F, P); ++s) n += ct_rows(1 << fft_bits(F, P, s)) * (1 << fft_bits_before(F, P, s));
+  return n;
+}
+constexpr int wave_fft_ct_n(int F, int T) { return fft_ct_n(wave_fft_fw(F, T), F / T); }
 
 template <int F, int T, typename Re, bool LTW1 = true, bool LTW2 = LTW1>
 struct WaveFft {
@@ -62,10 +70,15 @@ struct WaveFft {
   // LTW1: stage-1 twiddles from LDS (tw1); from four waves on (F 2048) also stage 2's rows
   // r = 3, 5, 6 (config 2 -0.5 %, LoS -0.8 %, MCNC -1.0 %, profiles/r03/ab_x; at F 1024 the
   // 3 KiB more would cost the third wave per SIMD)
-  using Sub = TeamFft<FW, 64, 1, Re, true, LTW1, LTW2 && (T / 64) >= 4>;
+  // fp64 with both LDS twiddle blocks: the twiddled radix-8 stages absorb their twiddles
+  // into FMAs (team_fft.h dft8_ct; the constants from the cot-tan region of the table)
+  using Sub = TeamFft<FW, 64, 1, Re, true, LTW1, LTW2 && (T / 64) >= 4, sizeof(Re) == 8>;
   static constexpr int TW1_N = Sub::TW1_N;
-  static constexpr int TWL_N = Sub::TWL_N;         // tw1: LDS copy of the entries Sub::twl_src names
-  static __device__ __forceinline__ int twl_src(int i) { return Sub::twl_src(i); }
+  static constexpr int TWL_N = Sub::TWL_N;         // tw1: LDS copy of the entries twl_src names
+  static __device__ __forceinline__ int twl_src(int i) {
+    return Sub::CT ? wave_fft_tw_total(F, T) + i : Sub::twl_src(i);
+  }
+  static_assert(!Sub::CT || Sub::CT_N == wave_fft_ct_n(F, T), "cot-tan table layout");
   static_assert(Sub::P == P, "sub-transform keeps the points per thread");
   static constexpr int ROW = Sub::LDS_ELEMS;
   static constexpr int LDS_TOTAL = WV * ROW;

@@ -11,7 +11,7 @@ import re
 import subprocess
 import tempfile
 
-CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+CSRC = os.environ.get("MIMO_CSRC") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                     "m-mimo-ofdm-with-nonlinear-pa-sim_amd", "csrc")
 ARGS = re.compile(r"trial_kernelI([df])Li(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d)ELb(\d)ELi(\d)ELi(\d)ELb(\d)")
 CH = {"1": "rayleigh", "2": "los", "3": "twopath", "4": "table"}
