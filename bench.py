@@ -311,7 +311,9 @@ def check_launch(world, rank):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    # ~5 s of kernel time at config 2: long enough for a device-activity sampler polling every
+    # few seconds to see the timed region (BENCH_r04 gpu_busy saw 0 samples of a 0.5-s region)
+    ap.add_argument("--steps", type=int, default=120)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1 << 16, help="trials (OFDM symbols) per GPU per step")
     ap.add_argument("--iters", type=str, default="0", help="receiver iterations, e.g. 0 or 0,1,2,3,4")

@@ -451,10 +451,21 @@ struct TeamFft {
     return s <= 1 ? 0 : ct_off(s - 1) + ct_rows(1 << fft_bits(F, P, s - 1)) * (1 << fft_bits_before(F, P, s - 1));
   }
   static constexpr int CT_N = CT ? ct_off(NST) : 0;  // cot-tan entries
-  static constexpr int TWL_N = CT && WAVE ? CT_N : TW1_N + (LTW2 ? 3 * NS2 : 0);  // entries of the LDS copy
+  // Which stages use them (MIMO_CT_TEAM for the team FFT: 1 all, 2 the radix-16 ones only,
+  // 0 none; the wave-local sub-transforms always all).  CT1: the team FFT's stage-1 constants
+  // from the caller's LDS copy (LTW1), the later stages' from global memory.
+#ifndef MIMO_CT_TEAM
+#define MIMO_CT_TEAM 1
+#endif
+  static constexpr bool ct_stage(int s) {
+    return CT && s >= 1 && (WAVE || MIMO_CT_TEAM == 1 || (MIMO_CT_TEAM == 2 && fft_bits(F, P, s) == 4));
+  }
+  static constexpr bool CT1 = !WAVE && LTW1 && ct_stage(1);
+  static constexpr int TWL_N = CT && WAVE ? CT_N : CT1 ? ct_off(2) : TW1_N + (LTW2 ? 3 * NS2 : 0);  // LDS copy
   // source index in the twiddle table of LDS-copy entry i < TWL_N (CT: relative to the
   // cot-tan region, which the caller's table places)
   static __host__ __device__ constexpr int twl_src(int i) {
+    if (CT1) return fft_tw_total(F, P) + i;  // the team table's cot-tan region, stage 1
     if ((CT && WAVE) || i < TW1_N) return i;
     const int j = i - TW1_N, row = j / NS2, r = row == 0 ? 3 : row == 1 ? 5 : 6;
     return fft_tw_off(F, P, 2) + r * NS2 + j % NS2;
@@ -500,7 +511,7 @@ struct TeamFft {
     for (int r = 0; r < R; ++r) v[r] = d[I + r * B];
     const int j = t + T * I;
     const int jm = j & (NS - 1);
-    if constexpr (CT && S >= 1) {
+    if constexpr (ct_stage(S)) {
       if constexpr (R == 8) {
         const C zc[4] = {w0[0], w0[1], w0[2], w0[3]};
         dft8_ct<DIR>(v, zc);
@@ -520,7 +531,7 @@ struct TeamFft {
 #pragma unroll
       for (int r = 1; r < R; ++r) v[r] = DIR < 0 ? cmul(v[r], w[r]) : cmulc(v[r], w[r]);
     }
-    if constexpr (!(CT && S >= 1)) Dft<R, DIR, (S == 0 ? bfly_mask(ZM, I, B, R) : 0u)>::run(v);
+    if constexpr (!ct_stage(S)) Dft<R, DIR, (S == 0 ? bfly_mask(ZM, I, B, R) : 0u)>::run(v);
     if constexpr (LAST) {
 #pragma unroll
       for (int r = 0; r < R; ++r) d[I + r * B] = v[r];
@@ -587,7 +598,7 @@ struct TeamFft {
     if constexpr (S < NST) {
       constexpr int R = 1 << bits(S);
       constexpr int NS = 1 << bits_before(S);
-      if constexpr (NS > 1 && !(LTW1 && S == 1) && !CT) {
+      if constexpr (NS > 1 && !(LTW1 && S == 1) && !ct_stage(S)) {
         constexpr int TW_OFF = fft_tw_off(F, P, S);
         const int jm0 = t & (NS - 1);
 #pragma unroll
@@ -610,11 +621,11 @@ struct TeamFft {
     static_assert(B >= 1 && B * R == P, "radix must divide points per thread");
     C* buf = lds + (NBUF == 2 ? ((S + PAR) & 1) * LDS_ELEMS : 0);
     C w0[R];
-    if constexpr (CT && S >= 1) {
+    if constexpr (ct_stage(S)) {
       // cot-tan constants in w0[0 .. ct_rows) (butterfly() runs dft8_ct / dft16_ct)
       static_assert(((T * (B - 1)) & (NS - 1)) == 0, "cot-tan stages: one twiddle set per thread");
       constexpr int Q = ct_rows(R);
-      if constexpr (WAVE) {
+      if constexpr (WAVE || (CT1 && S == 1)) {
         const C* cts = tw1 + ct_off(S) + (t & (NS - 1));
 #pragma unroll
         for (int q = 0; q < Q; ++q) w0[q] = cts[q * NS];
