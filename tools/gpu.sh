@@ -30,7 +30,7 @@ line() {  # line <name> <bench args...>
 
 lines() {
   local ws=("$@")
-  [ ${#ws[@]} -eq 0 ] && ws=(2 cnc4 2los 2twopath 2csi 2mcnc paper paper_cnc8 5su f32)
+  [ ${#ws[@]} -eq 0 ] && ws=(2 cnc4 2los 2twopath 2csi 2mcnc paper paper_cnc8 papercsi 5su f32)
   for w in "${ws[@]}"; do
     case $w in
       2) line 2 --steps 5 || return $? ;;
@@ -38,6 +38,7 @@ lines() {
       2mcnc) line 2mcnc --workload 2mcnc --iters 0,1,2 --batch 16384 --steps 3 || return $? ;;
       paper) line paper --workload paper --batch 32768 --steps 5 || return $? ;;
       paper_cnc8) line paper_cnc8 --workload paper --iters 0,1,2,3,4,5,6,7,8 --batch 32768 --steps 5 || return $? ;;
+      papercsi) line papercsi --workload papercsi --batch 32768 --steps 5 || return $? ;;
       5su) line 5su --workload 5su --batch 2048 --steps 3 || return $? ;;
       f32) line f32 --precision f32 --steps 5 || return $? ;;
       *) line $w --workload $w --steps 5 || return $? ;;
