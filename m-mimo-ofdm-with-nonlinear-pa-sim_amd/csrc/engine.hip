@@ -198,8 +198,6 @@ struct mimo_engine {
   double* d_tx_pos = nullptr;
   uint32_t* d_counts = nullptr;
   size_t counts_cap = 0;
-  char* d_csi_stage = nullptr;            // MIMO_CSI_STAGE builds only
-  size_t csi_stage_cap = 0;
   unsigned long long* d_tot = nullptr;    // [points][n_idx] totals of one run
   size_t tot_cap = 0;
   // per-launch tables in one device blob, filled by one copy from a pinned host buffer:
@@ -404,6 +402,7 @@ int ensure_device(mimo_engine* e) {
   // cot-tan constants of the twiddled stages (team_fft.h dft8_ct / dft16_ct), appended to a
   // stage table: (cos a, tan a) per (stage, row, lane); cos is never exactly 0 in double
   // (cos(pi/2) = 6.1e-17), so tan stays finite
+  // (appended for every instance; the kernels that do not run cot-tan stages never read them)
   auto append_ct = [](auto& tw, int Fs, int P, auto cvt) {
     for (int st = 1; st < mimo::fft_nst(Fs, P); ++st) {
       const int NS = 1 << mimo::fft_bits_before(Fs, P, st), R = 1 << mimo::fft_bits(Fs, P, st);
@@ -612,14 +611,6 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
     const uint64_t v = std::strtoull(env, nullptr, 10);
     if (v >= 1 && v < kChunk) kChunk = v;
   }
-#ifdef MIMO_CSI_STAGE
-  // experiment: CSI error terms staged per launch block, A x (NSLOT x T) complex values each
-  const size_t stage_per_block = (size_t)c.n_ant * (size_t)key.nslot * key.T * (key.f64 ? 16 : 8);
-  if (csi) {
-    kChunk = std::min<uint64_t>(kChunk, std::max<uint64_t>(1, (16ull << 30) / stage_per_block));
-    if (int rc = ensure_cap(e->d_csi_stage, e->csi_stage_cap, (size_t)kChunk * stage_per_block)) return rc;
-  }
-#endif
   struct Seg {
     int point;
     uint64_t first, n;
@@ -692,7 +683,6 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
     if (const char* env = std::getenv("MIMO_ABLATE")) base.ablate = (uint32_t)std::strtoul(env, nullptr, 0);
 #endif
     base.counts = e->d_counts;
-    base.csi_stage = reinterpret_cast<typename TP::C*>(e->d_csi_stage);
     base.chan_period = (uint32_t)std::max(0, c.chan_replay_period);
     // per-point parameter table (host), built once
     std::vector<TP> ptab(n_points, base);
@@ -820,7 +810,6 @@ void mimo_engine_destroy(mimo_engine* e) {
     (void)hipFree(e->d_tw[1]);
     (void)hipFree(e->d_f_rel);
     (void)hipFree(e->d_tw64);
-    if (e->d_csi_stage) (void)hipFree(e->d_csi_stage);
     if (e->d_twave64) (void)hipFree(e->d_twave64);
     if (e->d_twave32) (void)hipFree(e->d_twave32);
     (void)hipFree(e->d_lut64);

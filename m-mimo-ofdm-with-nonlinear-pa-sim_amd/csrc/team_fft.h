@@ -313,14 +313,16 @@ __device__ __forceinline__ void dft8_ct(C (&v)[8], const C (&zc)[4]) {
     bfly_ct<DIR, true>(a1[r0], a1[r0 + 2], zc[1], b[r0][1], b[r0][3]);
   }
   bfly_ct<DIR, false>(b[0][0], b[1][0], zc[2], v[0], v[4]);
-  bfly_ct<DIR, false>(b[0][1], b[1][1], zc[3], v[1], v[5]);
   bfly_ct<DIR, true>(b[0][2], b[1][2], zc[2], v[2], v[6]);
+  bfly_ct<DIR, false>(b[0][1], b[1][1], zc[3], v[1], v[5]);
   bfly_ct<DIR, true>(b[0][3], b[1][3], zc[3], v[3], v[7]);
 }
 // The same for R = 16 (four levels, 32 butterflies = 192 FMAs, against 15 complex
 // multiplies, the products forming 11 of the 15 twiddles and the ~152-op DFT-16): level 1
 // (r, r + 8) with z^8, level 2 (r, r + 4) with W4^k0 z^4, level 3 (r0, r0 + 2) with W8^m z^2,
 // level 4 (0, 1) with W16^m z.  zc: (c, t) of z^8, z^4, z^2, W8 z^2, z, W16 z, W8 z, W16^3 z.
+// (Forming the rotated rows from z^2 and z in registers instead -- 4 table rows, +2 ops on
+// 10 butterflies -- measured +1 to +4 %, profiles/r05/ab/ab_*_r05e.json: not taken.)
 template <int DIR, class C>
 __device__ __forceinline__ void dft16_ct(C (&v)[16], const C (&zc)[8]) {
   C a[2][8];
@@ -336,8 +338,8 @@ __device__ __forceinline__ void dft16_ct(C (&v)[16], const C (&zc)[8]) {
 #pragma unroll
   for (int r0 = 0; r0 < 2; ++r0) {
     bfly_ct<DIR, false>(b[r0][0], b[r0 + 2][0], zc[2], c[r0][0], c[r0][4]);
-    bfly_ct<DIR, false>(b[r0][1], b[r0 + 2][1], zc[3], c[r0][1], c[r0][5]);
     bfly_ct<DIR, true>(b[r0][2], b[r0 + 2][2], zc[2], c[r0][2], c[r0][6]);
+    bfly_ct<DIR, false>(b[r0][1], b[r0 + 2][1], zc[3], c[r0][1], c[r0][5]);
     bfly_ct<DIR, true>(b[r0][3], b[r0 + 2][3], zc[3], c[r0][3], c[r0][7]);
   }
 #pragma unroll
@@ -433,9 +435,6 @@ struct TeamFft {
   // fp64 F 2048 team's 3-teams-per-CU LDS line.)
   static constexpr bool LTW2 = LTW1 && LTW2_ON && NST >= 3 && fft_bits(F, P, 2) == 3;
   static constexpr int NS2 = NST >= 3 ? 1 << fft_bits_before(F, P, 2) : 1;
-  // CT (fp64, every stage >= 1 radix 8, both stages' constants in the LDS copy): the
-  // twiddled stages run dft8_ct on cot-tan constants, [4][NS] per stage (ct_off), which
-  // replace stage 1's block and stage 2's rows in the LDS copy.
   // CT (fp64): every twiddled stage (radix 8 or 16) runs dft8_ct / dft16_ct on cot-tan
   // constants, [ct_rows][NS] per stage at ct_off(s) of the cot-tan region: in the LDS copy
   // for the wave-local sub-transforms (which then replace stage 1's block and stage 2's
@@ -448,24 +447,17 @@ struct TeamFft {
   }
   static constexpr bool CT = CT_ON && sizeof(Re) == 8 && ct_ok() && (!WAVE || (LTW1 && LTW2 && NST == 3));
   static constexpr int ct_off(int s) {
-    return s <= 1 ? 0 : ct_off(s - 1) + ct_rows(1 << fft_bits(F, P, s - 1)) * (1 << fft_bits_before(F, P, s - 1));
+    return s <= 1 ? 0
+                  : ct_off(s - 1) + ct_rows(1 << fft_bits(F, P, s - 1)) * (1 << fft_bits_before(F, P, s - 1));
   }
   static constexpr int CT_N = CT ? ct_off(NST) : 0;  // cot-tan entries
-  // Which stages use them (MIMO_CT_TEAM for the team FFT: 1 all, 2 the radix-16 ones only,
-  // 0 none; the wave-local sub-transforms always all).  CT1: the team FFT's stage-1 constants
-  // from the caller's LDS copy (LTW1), the later stages' from global memory.
-#ifndef MIMO_CT_TEAM
-#define MIMO_CT_TEAM 1
-#endif
-  static constexpr bool ct_stage(int s) {
-    return CT && s >= 1 && (WAVE || MIMO_CT_TEAM == 1 || (MIMO_CT_TEAM == 2 && fft_bits(F, P, s) == 4));
-  }
-  static constexpr bool CT1 = !WAVE && LTW1 && ct_stage(1);
-  static constexpr int TWL_N = CT && WAVE ? CT_N : CT1 ? ct_off(2) : TW1_N + (LTW2 ? 3 * NS2 : 0);  // LDS copy
+  // (Team FFT variants measured and not taken, profiles/r05/ab/ab_*_r05e.json: the radix-16
+  // stages only, stage 1's constants from an LDS copy.)
+  static constexpr bool ct_stage(int s) { return CT && s >= 1; }
+  static constexpr int TWL_N = CT && WAVE ? CT_N : TW1_N + (LTW2 ? 3 * NS2 : 0);  // LDS copy
   // source index in the twiddle table of LDS-copy entry i < TWL_N (CT: relative to the
   // cot-tan region, which the caller's table places)
   static __host__ __device__ constexpr int twl_src(int i) {
-    if (CT1) return fft_tw_total(F, P) + i;  // the team table's cot-tan region, stage 1
     if ((CT && WAVE) || i < TW1_N) return i;
     const int j = i - TW1_N, row = j / NS2, r = row == 0 ? 3 : row == 1 ? 5 : 6;
     return fft_tw_off(F, P, 2) + r * NS2 + j % NS2;
@@ -625,7 +617,7 @@ struct TeamFft {
       // cot-tan constants in w0[0 .. ct_rows) (butterfly() runs dft8_ct / dft16_ct)
       static_assert(((T * (B - 1)) & (NS - 1)) == 0, "cot-tan stages: one twiddle set per thread");
       constexpr int Q = ct_rows(R);
-      if constexpr (WAVE || (CT1 && S == 1)) {
+      if constexpr (WAVE) {
         const C* cts = tw1 + ct_off(S) + (t & (NS - 1));
 #pragma unroll
         for (int q = 0; q < Q; ++q) w0[q] = cts[q * NS];

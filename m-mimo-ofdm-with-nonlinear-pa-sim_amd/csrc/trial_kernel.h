@@ -99,7 +99,6 @@ struct TrialParams {
   // scalar loads pair them as s_load_dwordx4; inserted after `seed` it cost the F 4096
   // instance 1 %, profiles/r04/misc/).
   uint64_t csi_seed;             // CH_TABLE + CSI: key of the one shared estimate (mimo_config.csi_seed)
-  C* csi_stage;                  // MIMO_CSI_STAGE builds: [launch block][A][NSLOT][T] CSI error terms
 };
 
 // Ablation switches for cost breakdowns.  Compiled in only with -DMIMO_ABLATION
@@ -657,12 +656,6 @@ struct Channel {
 };
 
 // ---------------------------------------------------------------- the kernel
-// Whether an FFT type reads stage-1 cot-tan constants from the kernel's LDS copy (team FFT).
-template <class FFTT, class = void>
-struct FFT_CT1 : std::false_type {};
-template <class FFTT>
-struct FFT_CT1<FFTT, std::void_t<decltype(FFTT::CT1)>> : std::integral_constant<bool, FFTT::CT1> {};
-
 // Occupancy tuning per instance (trial_inst.hip): MINW = waves/SIMD the register
 // allocation targets, NBUF = FFT exchange buffers (2: one barrier per exchange, 1: half
 // the LDS), SYMW_LDS = keep the pre-weighted symbols in LDS (thread-private) instead of
@@ -687,14 +680,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // stage 2's rows; fp64: the cot-tan constants of dft8_ct).  CSI instances too, since their
   // per-antenna power table is dynamic LDS sized by A (round 5; before, a static 4 KiB
   // table left no room for stage 2's rows at 3 teams per CU).
-  // fp64: the twiddled stages absorb their twiddles into FMAs (team_fft.h dft8_ct / dft16_ct);
-  // MIMO_CT_LDS1: the team FFT's stage-1 constants from an LDS copy
-#ifndef MIMO_CT_LDS1
-#define MIMO_CT_LDS1 0
-#endif
+  // fp64 up to F 4096: the twiddled stages absorb their twiddles into FMAs (team_fft.h
+  // dft8_ct / dft16_ct; F 4096 -1.0 to -1.6 %, CSI -7 to -12 %).  F 8192 keeps the stage
+  // twiddles with the prefetched bases: the cot-tan form measured +2.5 % there (its 16-point
+  // threads hold the extra constants live across the exchanges; profiles/r05/ab/ab_5su_r05e.json).
   using FFT = std::conditional_t<WAVEFFT, WaveFft<F, T, R, true, true>,
-                                 TeamFft<F, T, NBUF, R, false, MIMO_CT_LDS1 != 0 && sizeof(R) == 8 && F == 4096, false,
-                                         sizeof(R) == 8>>;
+                                 TeamFft<F, T, NBUF, R, false, false, false, sizeof(R) == 8 && F <= 4096>>;
   using SL = Slots<F, T, NSLOT, ALIGNED>;
   using CHN = Channel<R, F, T, NSLOT, ALIGNED, CH>;
   constexpr int P = FFT::P;
@@ -717,7 +708,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   __shared__ C symw_s[SYMW_LDS ? NSLOT * T : 1];  // [slot][thread]
   // wave-split FFT: the one-wave sub-transforms read stage 1's twiddles and (without CSI)
   // stage 2's rows r = 3, 5, 6 from LDS (team_fft.h TWL_N; -24 f64 ops per antenna at config 2)
-  constexpr bool LTW1 = WAVEFFT || FFT_CT1<FFT>::value;
+  constexpr bool LTW1 = WAVEFFT;
   constexpr int TW1_N = [] {
     if constexpr (LTW1) return FFT::TWL_N; else return 1;
   }();
@@ -842,13 +833,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       C zc[NSLOT];
       CHN::normals(csi_key, csi_trial, ST_CSI, (uint32_t)a, tl, S, zc);
       const R sc = p.csi_b * sqrt_ieee(pw);
-#ifdef MIMO_CSI_STAGE
-      {  // experiment: the error term staged through HBM for the array pass
-        C* st = p0.csi_stage + (((size_t)blockIdx.x * A + a) * NSLOT) * T + tl;
-#pragma unroll
-        for (int s = 0; s < NSLOT; ++s) st[s * T] = mkc(sc * zc[s].x, sc * zc[s].y);
-      }
-#endif
       if (clean_cc) {
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s) {
@@ -1016,21 +1000,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       auto hfill_fft = [&](int w) __attribute__((always_inline)) { hfill(FFT::XCHG + w); };
       C he[CSI ? NSLOT : 1];
       if constexpr (CSI) {
-#ifdef MIMO_CSI_STAGE
-        const C* st = p0.csi_stage + (((size_t)blockIdx.x * A + a) * NSLOT) * T + tl;
-#pragma unroll
-        for (int s = 0; s < NSLOT; ++s) {
-          const C ez = st[s * T];
-          he[s] = mkc(fmar(p.csi_a, h[s].x, ez.x), fmar(p.csi_a, h[s].y, ez.y));
-        }
-#else
+        // (regenerated, not staged: the error term written to HBM in pass 1 and read back
+        // here measured +11 %, profiles/r05/ab/ab_2csi_stage_r05e.json)
         C zc[NSLOT];
         CHN::normals(csi_key, csi_trial, ST_CSI, (uint32_t)a, tl, S, zc);
         const R sc = p.csi_b * sqrt_ieee(pw_csi[a]);
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s)
           he[s] = mkc(fmar(p.csi_a, h[s].x, sc * zc[s].x), fmar(p.csi_a, h[s].y, sc * zc[s].y));
-#endif
       }
       auto hest = [&](int s) __attribute__((always_inline)) -> C {
         if constexpr (CSI) return he[s]; else return h[s];
