@@ -423,6 +423,19 @@ int ensure_device(mimo_engine* e) {
   auto to_f64 = [](double c, double s) { return make_double2(c, s); };
   std::vector<float2> tws[2] = {twiddles(mimo::team_size(F), to_f32), twiddles(mimo::alt_team_size(F), to_f32)};
   std::vector<double2> tw64 = twiddles(mimo::team_size64(F), to_f64);
+  // split FFT (split_fft.h): the F/2-point sub-transform's table, its cot-tan region, then
+  // the radix-2 stage's (cos a, tan a), a = -2 pi n / F, n < F/2
+  if (mimo::split_fft_used(F, mimo::team_size64(F), true)) {
+    const int T = mimo::team_size64(F), P = F / T;
+    tw64 = twiddles_of(F / 2, T / 2, to_f64);
+    tw64.resize(mimo::fft_tw_total(F / 2, P));
+    if (mimo::kSplitCt) append_ct(tw64, F / 2, P, to_f64);
+    for (int n = 0; n < F / 2; ++n) {
+      const double a = -2.0 * M_PI * (double)n / (double)F, c = std::cos(a);
+      tw64.push_back(make_double2(c, std::sin(a) / c));
+    }
+    if ((int)tw64.size() != mimo::split_fft_tw_total(F, T)) return MIMO_ENOKERNEL;  // table and kernel disagree
+  }
   // wave-split FFT (wave_fft.h): the one-wave sub-transform's stages, then exp(-j 2 pi n / F)
   auto wave_twiddles = [&](int T, auto cvt) {
     auto tw = twiddles_of(mimo::wave_fft_fw(F, T), 64, cvt);

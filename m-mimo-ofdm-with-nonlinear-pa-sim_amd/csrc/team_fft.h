@@ -351,6 +351,12 @@ __device__ __forceinline__ void dft16_ct(C (&v)[16], const C (&zc)[8]) {
 // Host / device: the cot-tan rows of a radix-R stage (R = 8: 4 rows, 16: 8 rows), lane jm,
 // z = exp(-j 2 pi jm / (R NS)), as angles in revolutions (ct_rows, ct_rev).
 __host__ __device__ constexpr int ct_rows(int R) { return R == 8 ? 4 : 8; }
+// entries of a transform's cot-tan region: stage s >= 1, [ct_rows][NS_s] (c, tan) each
+constexpr int fft_ct_n(int F, int P) {
+  int n = 0;
+  for (int s = 1; s < fft_nst(F, P); ++s) n += ct_rows(1 << fft_bits(F, P, s)) * (1 << fft_bits_before(F, P, s));
+  return n;
+}
 __host__ __device__ constexpr double ct_rev(int R, int ns, int jm, int q) {
   const double th = -(double)jm / ((double)R * ns);
   if (R == 8) return q == 0 ? 4 * th : q == 1 ? 2 * th : q == 2 ? th : th - 0.125;
@@ -690,6 +696,8 @@ struct TeamFft {
   }
 
   static constexpr int XCHG = NST - 1;  // exchanges per transform
+  // The frequency-domain vector is cyclic in the thread id itself (split_fft.h permutes it).
+  static __device__ __forceinline__ int freq_thread(int t) { return t; }
   static constexpr int LDS_TOTAL = NBUF * LDS_ELEMS;  // exchange buffer(s)
 
   // Un-normalised transform of the team's cyclic-distributed vector.  Ends with the

@@ -34,6 +34,7 @@
 #include "philox.h"
 #include "team_fft.h"
 #include "wave_fft.h"
+#include "split_fft.h"
 
 namespace mimo {
 
@@ -684,8 +685,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // dft8_ct / dft16_ct; F 4096 -1.0 to -1.6 %, CSI -7 to -12 %).  F 8192 keeps the stage
   // twiddles with the prefetched bases: the cot-tan form measured +2.5 % there (its 16-point
   // threads hold the extra constants live across the exchanges; profiles/r05/ab/ab_5su_r05e.json).
-  using FFT = std::conditional_t<WAVEFFT, WaveFft<F, T, R, true, true>,
-                                 TeamFft<F, T, NBUF, R, false, false, false, sizeof(R) == 8 && F <= 4096>>;
+  // fp64 F 8192: two 4096-point sub-transforms and a radix-2 stage through lane-half swaps
+  // (split_fft.h: two LDS exchanges per transform instead of three)
+  constexpr bool SPLITFFT = split_fft_used(F, T, sizeof(R) == 8);
+  using FFT = std::conditional_t<
+      WAVEFFT, WaveFft<F, T, R, true, true>,
+      std::conditional_t<SPLITFFT, SplitFft<F, T, NBUF, R>,
+                         TeamFft<F, T, NBUF, R, false, false, false, sizeof(R) == 8 && F <= 4096>>>;
   using SL = Slots<F, T, NSLOT, ALIGNED>;
   using CHN = Channel<R, F, T, NSLOT, ALIGNED, CH>;
   constexpr int P = FFT::P;
@@ -700,6 +706,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   __shared__ C lds[FFT::LDS_TOTAL];
   __shared__ R red[T / 64];  // sized by the team
   __shared__ R vk_part[2][T / 64];
+  // alpha formed by one wave per antenna (array_pass): config 2 -1.0 %, CSI -1.2 %, config-5
+  // array -2.3 %; the 16-point F 4096 team +0.8 % (its register allocation again), so not
+  // there (profiles/r05/ab/ab_*_alpha1.json).  MIMO_ALPHA1=0: every wave forms it.
+#ifndef MIMO_ALPHA1
+#define MIMO_ALPHA1 1
+#endif
+  constexpr bool ALPHA1 = MIMO_ALPHA1 != 0 && F != 4096;
+  __shared__ R alpha_s[2];
   // per-antenna mean |H|^2 (CSI model): dynamic LDS of A doubles (the launch sizes it), not
   // a static kMaxCsiAnt table -- the static 4 KiB cost F 4096 its second team per CU and F
   // 2048 its stage-2 twiddle rows (and with them the cot-tan FFT stages)
@@ -717,6 +731,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 
   const int t = threadIdx.x;
   const bool t0 = (t == 0);
+  // the thread's sub-carriers: bins tf + T m of the FFT's frequency layout (tf = t except for
+  // the split FFT, whose layout is cyclic in a permuted thread index; tf = 0 iff t = 0)
+  const int tf = FFT::freq_thread(t);
   const int lane = t & 63, wid = t >> 6;
   const uint32_t trial = (uint32_t)(p.first_trial + (blockIdx.x - p0.point_start[pi]));
   const Key key{(uint32_t)p.seed, (uint32_t)(p.seed >> 32)};
@@ -767,7 +784,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 #pragma unroll
   for (int s = 0; s < NSLOT; ++s) {
     bool v;
-    SL::k_of(s, t, S, v);
+    SL::k_of(s, tf, S, v);
     valid_mask |= (v ? 1u : 0u) << s;
   }
 
@@ -779,7 +796,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       return R(1);
     } else {
       bool v;
-      const int k = SL::k_of(s, opaque(t), S, v);
+      const int k = SL::k_of(s, opaque(tf), S, v);
       return v ? p.f_rel[k] : R(1);
     }
   };
@@ -800,7 +817,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   const bool clean_cc = CSI && p.incl_clean;
   for (int a = 0; a < (MIMO_ABL(p, ABL_PASS1) ? 1 : A); ++a) {
     MIMO_ISA_MARK("pass1");
-    const int tl = opaque(t);
+    const int tl = opaque(tf);
     if constexpr (CH == CH_RAYLEIGH && !CSI) {
       if (!MIMO_ABL(p, ABL_RNG)) {
         R e2[NSLOT];
@@ -963,12 +980,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     C hnext[PIPE ? NSLOT : 1];
     if constexpr (PIPE) {
       const R sa = p.ant_rel[0];
-      if (MIMO_ABL(p, ABL_RNG)) CHN::template gen<FREL>(p, key, ch_trial, 0, t, rx, hnext);
-      else CHN::normals(key, ch_trial, ST_CHAN, 0u, t, S, hnext, bm_c<R>(sa * sa));
+      if (MIMO_ABL(p, ABL_RNG)) CHN::template gen<FREL>(p, key, ch_trial, 0, tf, rx, hnext);
+      else CHN::normals(key, ch_trial, ST_CHAN, 0u, tf, S, hnext, bm_c<R>(sa * sa));
     }
     for (int a = 0; a < A; ++a) {
       MIMO_ISA_MARK("array_pass");
-      const int tl = opaque(t);
+      const int tl = opaque(tf);
       C h[NSLOT];
       if constexpr (PIPE) {
 #pragma unroll
@@ -1043,17 +1060,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
         FFT::template run<+1, 0, SL::zero_mask()>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_ifft,
                                                   tw1);
       if (!MIMO_ABL(p, ABL_PA)) pa_block<COLD_OUT>(p.pa_kind, d, p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
-      if (!MIMO_ABL(p, ABL_FFT))
-        FFT::template run_second<-1>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_fft, tw1);
-      if constexpr (PIPE) {
-        if (MIMO_ABL(p, ABL_FFT)) {  // no transforms ran, so no exchange windows (ABL_XCHG keeps them)
-#pragma unroll
-          for (int w = 0; w < 2 * FFT::XCHG; ++w) hfill(w);
-        }
-      }
-      if (MIMO_ABL(p, ABL_FFT)) __syncthreads();  // keep the vk_part hand-off ordered
-      R alpha_a = R(0);
-      if (main_pass) {
+      // alpha_a (Bussgang gain of antenna a's PA from its precoding power, main pass only)
+      auto alpha_of_vk = [&]() __attribute__((always_inline)) -> R {
         R vks = vk_part[a & 1][0];
 #pragma unroll
         for (int i = 1; i < W; ++i) vks += vk_part[a & 1][i];
@@ -1064,7 +1072,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
           R acc = p.apoly[8];
 #pragma unroll
           for (int i = 7; i >= 0; --i) acc = fmar(acc, x, p.apoly[i]);
-          alpha_a = acc;
+          return acc;
         } else if (sizeof(R) == 8 && absr(x) <= p.alpha_xlim) {
           // Horner, 18 FMAs with the coefficients as SGPR operands instead of the library
           // exp + erfc.  (Plain fma() compiles to v_fmac_f64 and copies every coefficient
@@ -1076,15 +1084,37 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
             const double ck = p.amono64[k];
             asm("v_fma_f64 %0, %1, %2, %3" : "=v"(acc) : "v"(acc), "v"((double)x), "s"(ck));
           }
-          alpha_a = (R)acc;
+          return (R)acc;
         } else {
           // (the register-diet pass sums vk / F: vks F is the precoding power)
           const R g2 = p.alpha_c / (PRE_EW ? vks * (R)F : vks);
           // fp64: the segment table (alpha_fit.h, appended to the Box-Muller tables in HBM)
-          if constexpr (COLD_OUT) alpha_a = alpha_seg(g2, reinterpret_cast<const double*>(p.lut + kLut64));
-          else alpha_a = alpha_of_gamma2(g2);
+          if constexpr (COLD_OUT) return alpha_seg(g2, reinterpret_cast<const double*>(p.lut + kLut64));
+          else return alpha_of_gamma2(g2);
+        }
+      };
+      // ALPHA1: one wave per antenna (a mod W) forms it from the vk partials (visible since the
+      // IFFT's first barrier) and hands it over in LDS; the forward FFT's cross-wave barrier
+      // orders the hand-off (alpha_s double-buffered like vk_part).  The other waves skip the
+      // partial sum and the 18-FMA polynomial.
+      if constexpr (ALPHA1) {
+        if (main_pass && wid == (a & (W - 1))) {
+          const R al = alpha_of_vk();
+          if (lane == 0) alpha_s[a & 1] = al;
         }
       }
+      if (!MIMO_ABL(p, ABL_FFT))
+        FFT::template run_second<-1>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_fft, tw1);
+      if constexpr (PIPE) {
+        if (MIMO_ABL(p, ABL_FFT)) {  // no transforms ran, so no exchange windows (ABL_XCHG keeps them)
+#pragma unroll
+          for (int w = 0; w < 2 * FFT::XCHG; ++w) hfill(w);
+        }
+      }
+      // keep the vk_part / alpha_s hand-offs ordered when the ablations drop the barriers
+      if (MIMO_ABL(p, ABL_FFT) || (ALPHA1 && MIMO_ABL(p, ABL_XCHG))) __syncthreads();
+      R alpha_a = R(0);
+      if (main_pass) alpha_a = ALPHA1 ? alpha_s[a & 1] : alpha_of_vk();
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
         const C y = SL::gather(d, s, t0);
@@ -1108,18 +1138,18 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 
   {
     uint32_t lab0[NSLOT];
-    gen_labels(t, lab0);
+    gen_labels(tf, lab0);
     set_symbols(lab0);
   }
   array_pass(true, r);
 #pragma unroll
   for (int s = 0; s < NSLOT; ++s) g[s] *= inv_nrm[s];
   uint32_t lab[NSLOT];
-  gen_labels(opaque(t), lab);
+  gen_labels(opaque(tf), lab);
 
   // ---- AWGN + AGC (noise.py:56-83 on all bins; only in-band bins matter)
   C zn[NSLOT];
-  CHN::normals(key, trial, ST_NOISE, 0u, t, S, zn);
+  CHN::normals(key, trial, ST_NOISE, 0u, tf, S, zn);
   R eta_p = R(0);
 #pragma unroll
   for (int s = 0; s < NSLOT; ++s) {

@@ -50,13 +50,8 @@ constexpr bool wave_fft_used(int F, int T, bool f64) {
 constexpr int wave_fft_fw(int F, int T) { return F / (T / 64); }
 constexpr int wave_fft_tw_inter(int F, int T) { return fft_tw_total(wave_fft_fw(F, T), F / T); }
 constexpr int wave_fft_tw_total(int F, int T) { return wave_fft_tw_inter(F, T) + F; }
-// The fp64 sub-transforms' cot-tan constants (team_fft.h dft8_ct) follow the inter twiddles:
-// stage s >= 1: [ct_rows][NS_s] entries (c, tan) (ct_rev).  Their count:
-constexpr int fft_ct_n(int F, int P) {
-  int n = 0;
-  for (int s = 1; s < fft_nst(F, P); ++s) n += ct_rows(1 << fft_bits(F, P, s)) * (1 << fft_bits_before(F, P, s));
-  return n;
-}
+// The fp64 sub-transforms' cot-tan constants (team_fft.h dft8_ct) follow the inter twiddles
+// (fft_ct_n entries).
 constexpr int wave_fft_ct_n(int F, int T) { return fft_ct_n(wave_fft_fw(F, T), F / T); }
 
 template <int F, int T, typename Re, bool LTW1 = true, bool LTW2 = LTW1>
@@ -86,6 +81,7 @@ struct WaveFft {
   static constexpr int TW_INTER = wave_fft_tw_inter(F, T);
 
   using NoFill = typename Sub::NoFill;
+  static __device__ __forceinline__ int freq_thread(int t) { return t; }  // cyclic in t
 
   // Zero mask of radix-WV butterfly i's inputs v[n1] = d[i + NB n1] from the register mask.
   static constexpr uint32_t bfly_mask(uint32_t zm, int i) {
