@@ -967,6 +967,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       return symw_r[s];
     }
   };
+  // WSC: the weight w = 1 / ||Hhat|| / sqrt(F) per slot is what the antenna loops hold
+  // (1 / ||Hhat|| is rederived from it after the main pass): no per-antenna multiply and no
+  // laundering copy of 1 / ||Hhat||, 8 VALU per antenna: config 2 -0.2 %, MCNC -0.6 %, but the
+  // CSI instance +5.3 % (its allocation again), so not with CSI (profiles/r05/ab/ab_*_wsc.json).
+  constexpr bool WSC = PRE_EW && !CSI;
+  R wsc[WSC ? NSLOT : 1];
   auto array_pass = [&](bool main_pass, C (&acc)[NSLOT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) acc[s] = czero<R>();
@@ -1039,9 +1045,15 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
           // the lattice point times conj(Hhat w), w = 1 / ||Hhat|| / sqrt(F): vk accumulates
           // |Hhat w|^2 = |Hhat|^2 / ||Hhat||^2 / F directly (11 f64 ops per slot, not 13;
           // vk_scale restores the factor F)
-          R in = inv_nrm[s];
-          asm volatile("" : "+v"(in));
-          const C ew = cscale(e, in * inv_sqrt_f);
+          R in;
+          if constexpr (WSC) {
+            in = wsc[s];
+          } else {
+            in = inv_nrm[s];
+            asm volatile("" : "+v"(in));
+            in *= inv_sqrt_f;
+          }
+          const C ew = cscale(e, in);
           x[s] = cmulc(slab_point(s), ew);
           vk = fmar(ew.x, ew.x, fmar(ew.y, ew.y, vk));
           if constexpr (!E2_RE) e2[s] = fmar(e.x, e.x, e.y * e.y);
@@ -1141,7 +1153,15 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     gen_labels(tf, lab0);
     set_symbols(lab0);
   }
+  if constexpr (WSC) {
+#pragma unroll
+    for (int s = 0; s < NSLOT; ++s) wsc[s] = inv_nrm[s] * inv_sqrt_f;
+  }
   array_pass(true, r);
+  if constexpr (WSC) {
+#pragma unroll
+    for (int s = 0; s < NSLOT; ++s) inv_nrm[s] = wsc[s] / inv_sqrt_f;
+  }
 #pragma unroll
   for (int s = 0; s < NSLOT; ++s) g[s] *= inv_nrm[s];
   uint32_t lab[NSLOT];
