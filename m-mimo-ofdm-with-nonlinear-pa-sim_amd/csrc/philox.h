@@ -115,8 +115,9 @@ __device__ __forceinline__ float bm_log(uint32_t w0, float) {
 // fp64: LDS-table ln (real.h ln_unit; the trial kernel loads lut64 first).  The series
 // forms (ln_pos, sincos_rev) measured 1.4-3.9 % slower.
 __device__ __forceinline__ double bm_log(uint32_t w0, double) {
-  const double u1 = ((double)w0 + 0.5) * 2.3283064365386963e-10;  // exact argument
-  return ln_unit(u1);
+  // ln of u1 = (w0 + 0.5) 2^-32 from the bits of w0 + 0.5 (exact) with the 2^-32 taken into
+  // ln_unit's exponent: no scaling instruction
+  return ln_unit<-32>((double)w0 + 0.5);
 }
 
 __device__ __forceinline__ float2 box_muller(uint32_t w0, uint32_t w1, float c = kNegLn2) {

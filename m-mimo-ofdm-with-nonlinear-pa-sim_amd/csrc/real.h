@@ -136,9 +136,11 @@ __device__ __forceinline__ void sincos_rev_lut(double r, double& sn, double& cs)
 // (the top 9 mantissa bits, width 2^-10) gives c_i ~ 1 / centre_i (12 bits; c = 1 for the
 // top bucket: t = m - 1 exactly as u -> 1), t = m c_i - 1 with |t| < 2^-10, and
 // log1p(t) to t^6 (truncation < 2^-60 relative).
+// ESC: ln(x 2^ESC) -- the scale enters the exponent only (Box-Muller: x = w0 + 0.5, ESC = -32).
+template <int ESC = 0>
 __device__ __forceinline__ double ln_unit(double x) {
   const uint32_t hi = (uint32_t)__double2hiint(x), lo = (uint32_t)__double2loint(x);
-  const int e = (int)(hi >> 20) - 1022;
+  const int e = (int)(hi >> 20) - 1022 + ESC;
   const double m = __hiloint2double((int)((hi & 0xFFFFFu) | 0x3FE00000u), (int)lo);
   const double2 cl = lut64[(hi >> 11) & 511u];
   const double t = fma(m, cl.x, -1.0);
