@@ -876,6 +876,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     const R fr = frel_of(s);
     etac_p += v ? nrm2[s] * (fr * fr) : R(0);
   }
+  // etac_p is used only by the clean run after the array pass: pinned here, or the compiler
+  // sinks its sum into that conditional block and carries nrm2 and f_rel (16 doubles at
+  // F 8192) across the antenna loop -- spilled once per trial
+  asm volatile("" : "+v"(etac_p));
   if constexpr (CSI) __syncthreads();  // pw_csi visible
 
   C d[P];
