@@ -529,6 +529,29 @@ struct Channel {
     }
   }
 
+  // Polar form of normals() (aligned instances): rho^2 = c ln u1 and the angle word w1 of
+  // every slot's draw (the draw is rho e^{j 2 pi w1 2^-32}, box_muller), no sqrt / sin / cos.
+  // fn(slot, rho^2, angle word) per slot, one Philox call (two slots) at a time.
+  template <class Fn>
+  static __device__ __forceinline__ void polar(Key key, uint32_t trial, uint32_t stream, uint32_t aux, int t, int S, R c,
+                                               const Fn& fn) {
+    static_assert(ALIGNED, "aligned slot map");
+    constexpr int Q = SL::HALF / 2;
+    const bool t0 = (t == 0);
+    const int qp = (S >> 2) - 1 + t;
+#pragma unroll
+    for (int j = 0; j < Q; ++j) {
+      const bool sw = (j == 0) && t0;
+      uint4 w = philox4x32_10<kUni>(make_uint4(sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, stream, aux),
+                                    key);
+      fn(j, c * bm_log(sw ? w.z : w.x, R(0)), sw ? w.w : w.y);
+      fn(j + Q, c * bm_log(sw ? w.x : w.z, R(0)), sw ? w.y : w.w);
+      w = philox4x32_10<kUni>(make_uint4((uint32_t)(t + T * j), trial, stream, aux), key);
+      fn(SL::HALF + j, c * bm_log(w.x, R(0)), w.y);
+      fn(SL::HALF + j + Q, c * bm_log(w.z, R(0)), w.w);
+    }
+  }
+
   // |H|^2 of antenna a at the thread's slots for the closed-form channels (gen<false>'s
   // magnitudes, for pass 1's MRT norms): LoS |a1 e^{j phi1}|^2 = a1^2 -- no phase at all;
   // two-path |a1 e^{j phi1} - a2 e^{j phi2}|^2 = (a1 - a2)^2 + 4 a1 a2 sin^2((phi1 - phi2) / 2)
@@ -815,6 +838,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     if constexpr (CSI) cc[s] = czero<R>();
   }
   const bool clean_cc = CSI && p.incl_clean;
+  // pass 1 of the Rayleigh CSI instances in polar form (below; MIMO_CSI_POLAR=0: Cartesian)
+#ifndef MIMO_CSI_POLAR
+#define MIMO_CSI_POLAR 1
+#endif
+  constexpr bool CSI_POLAR = MIMO_CSI_POLAR != 0 && CSI && CH == CH_RAYLEIGH && ALIGNED && sizeof(R) == 8;
   for (int a = 0; a < (MIMO_ABL(p, ABL_PASS1) ? 1 : A); ++a) {
     MIMO_ISA_MARK("pass1");
     const int tl = opaque(tf);
@@ -832,6 +860,39 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       CHN::power_closed(p, a, tl, rx, e2);
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) nrm2[s] += e2[s];
+      continue;
+    }
+    if constexpr (CSI_POLAR) {
+      // Rayleigh + CSI in polar form: with h = rho_h e^{j phi_h} (the FSPL ratio f_c / f_k in
+      // rho_h), z = rho_z e^{j phi_z} and Hhat = a h + sc z,
+      // |Hhat|^2 = a^2 rho_h^2 + sc^2 rho_z^2 + 2 a sc rho_h rho_z cos(phi_h - phi_z)
+      // and h conj(Hhat) = a rho_h^2 + sc rho_h rho_z e^{j (phi_h - phi_z)}: one sine / cosine of
+      // the angle words' difference (exact mod 2^32) and one sqrt per slot instead of two full
+      // Box-Muller draws and the complex products (mp_model.py:264-282 restated).
+      R rh2[NSLOT];
+      uint32_t ah[NSLOT];
+      const R sa = p.ant_rel[a];
+      R pw = R(0);
+      CHN::polar(key, ch_trial, ST_CHAN, (uint32_t)a, tl, S, bm_c<R>(sa * sa),
+                 [&](int s, R r2, uint32_t w1) __attribute__((always_inline)) {
+                   bool v;
+                   const R fr = p.f_rel[SL::k_of(s, tl, S, v)];  // H keeps f_c / f_k with CSI (gen<true>)
+                   rh2[s] = r2 * (fr * fr);
+                   ah[s] = w1;
+                   pw += rh2[s];
+                 });
+      pw = team_sum<T>(pw, red) / (R)S;
+      if (t0) pw_csi[a] = pw;
+      const R sc = p.csi_b * sqrt_ieee(pw), ca = p.csi_a;
+      CHN::polar(csi_key, csi_trial, ST_CSI, (uint32_t)a, tl, S, bm_c<R>(R(1)),
+                 [&](int s, R rz2, uint32_t wz) __attribute__((always_inline)) {
+                   const R rhz = sqrt_n1(rh2[s] * rz2);  // both > 0: u1 < 1 always
+                   R sn, cs;
+                   sincos_lut(ah[s] - wz, sn, cs);
+                   const R tz = sc * rhz;
+                   nrm2[s] = fmar(ca * ca, rh2[s], fmar(sc * sc, rz2, fmar(R(2) * ca * tz, cs, nrm2[s])));
+                   if (clean_cc) cc[s] = cadd(cc[s], mkc(fmar(ca, rh2[s], tz * cs), tz * sn));
+                 });
       continue;
     }
     C h[NSLOT];
