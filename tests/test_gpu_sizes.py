@@ -64,23 +64,26 @@ def test_sizes_vs_oracle(monkeypatch, F, S, A, M, pa, p, ibo, team, prec):
 
 
 CONFIG5 = [
-    # A,  M,  pa,        p,   ibo, channel,    receiver, trials
-    (256, 64, "rapp", 3.0, 3.0, "rayleigh", "cnc", 6),    # config-5 array geometry (one user)
-    (8, 16, "softlim", 0.0, 1.0, "rayleigh", "mcnc", 8),  # MCNC array passes through the F 8192 path
-    (16, 16, "softlim", 0.0, 2.0, "los", "cnc", 8),       # closed-form LoS on the F 8192 path
+    # A,  M,  pa,        p,   ibo, channel,    receiver, trials, csi
+    (256, 64, "rapp", 3.0, 3.0, "rayleigh", "cnc", 6, None),    # config-5 array geometry (one user)
+    (8, 16, "softlim", 0.0, 1.0, "rayleigh", "mcnc", 8, None),  # MCNC array passes through the F 8192 path
+    (16, 16, "softlim", 0.0, 2.0, "los", "cnc", 8, None),       # closed-form LoS on the F 8192 path
+    (8, 16, "softlim", 0.0, 2.0, "rayleigh", "cnc", 8, 0.2),    # CSI (polar pass 1) on the F 8192 path
 ]
 
 
 @pytest.mark.parametrize("prec", PRECISIONS)
-@pytest.mark.parametrize("A,M,pa,p,ibo,channel,receiver,n", CONFIG5)
-def test_config5_array_vs_oracle(A, M, pa, p, ibo, channel, receiver, n, prec):
+@pytest.mark.parametrize("A,M,pa,p,ibo,channel,receiver,n,csi", CONFIG5)
+def test_config5_array_vs_oracle(A, M, pa, p, ibo, channel, receiver, n, csi, prec):
     """BASELINE config 5's array at one user (256 antennas, F 8192, 4096 sub-carriers,
-    Rapp p = 3) and the other F 8192 receivers / channels: per-trial counts EXACTLY equal to
-    the oracle's.  The fp64 instance is the 512-thread team (T = 512, 16 points per thread,
-    radix 8.8.8.16 TeamFft, per-slot state in registers), as eng.describe() prints."""
+    Rapp p = 3) and the other F 8192 receivers / channels / CSI: per-trial counts EXACTLY
+    equal to the oracle's.  The fp64 instance is the 512-thread team (T = 512, 16 points per
+    thread) on the split FFT (split_fft.h: two 4096-point sub-transforms and a lane-swap
+    radix-2 stage), as eng.describe() prints."""
     F, S = 8192, 4096
     snr = float(sim.rm.ebn0_to_snr(15.0, S, S, M))
-    cfg = sim.SimConfig(A, S, F, M, pa=pa, p_hardness=p, ibo_db=ibo, snr_db=snr, channel=channel, receiver=receiver)
+    cfg = sim.SimConfig(A, S, F, M, pa=pa, p_hardness=p, ibo_db=ibo, snr_db=snr, channel=channel, receiver=receiver,
+                        csi_eps=csi)
     iters = [0, 1, 2]
     ref = sim.run_trials(cfg, 77, np.arange(n), iters=iters, incl_clean=True, chunk=2)
     eng = engine_for(cfg, precision=prec)
@@ -100,6 +103,8 @@ BENCH_GEOMETRIES = [
     (4096, 2048, "rayleigh", "cnc", 0.1),
     (4096, 2048, "rayleigh", "mcnc", None),
     (4096, 2048, "two_path", "mcnc", None),
+    (512, 256, "rayleigh", "cnc", 0.3),  # a one-wave CSI instance (polar pass 1 at T = 64)
+    (1024, 512, "rayleigh", "mcnc", 0.2),  # MCNC with CSI (the estimate in every array pass)
 ]
 
 
