@@ -97,7 +97,8 @@ static __shared__ double2 lut64[kLut64];
 // multiply fewer than forming phi = h f first.
 __device__ __forceinline__ void sincos_lut(uint32_t w, double& sn, double& cs) {
   const uint32_t i = (w + 0x800000u) >> 24;  // wraps to 0 near a full revolution
-  const double f = (double)(int)(w - (i << 24));  // [-2^23, 2^23), exact
+  // w - i 2^24 = the low 24 bits of w sign-extended (one v_bfe_i32), in [-2^23, 2^23)
+  const double f = (double)(((int)(w << 8)) >> 8);
   constexpr double h = 1.4629180792671596e-09;    // 2 pi 2^-32
   constexpr double h2 = h * h;
   const double z = f * f;                         // exact (< 2^46)
@@ -139,9 +140,11 @@ __device__ __forceinline__ void sincos_rev_lut(double r, double& sn, double& cs)
 // ESC: ln(x 2^ESC) -- the scale enters the exponent only (Box-Muller: x = w0 + 0.5, ESC = -32).
 template <int ESC = 0>
 __device__ __forceinline__ double ln_unit(double x) {
-  const uint32_t hi = (uint32_t)__double2hiint(x), lo = (uint32_t)__double2loint(x);
-  const int e = (int)(hi >> 20) - 1022 + ESC;
-  const double m = __hiloint2double((int)((hi & 0xFFFFFu) | 0x3FE00000u), (int)lo);
+  // m and e by v_frexp_mant / v_frexp_exp (x normal, > 0): two instructions instead of the
+  // bit surgery (shift, add; and, or and a register copy); the bucket from x's top mantissa bits
+  const double m = __builtin_amdgcn_frexp_mant(x);
+  const int e = __builtin_amdgcn_frexp_exp(x) + ESC;
+  const uint32_t hi = (uint32_t)__double2hiint(x);
   const double2 cl = lut64[(hi >> 11) & 511u];
   const double t = fma(m, cl.x, -1.0);
   double q = -1.0 / 6;
