@@ -552,6 +552,33 @@ struct Channel {
     }
   }
 
+  // normals() with a per-slot scale folded into the Box-Muller radius: z = (rho w_s) e^{j phi}
+  // and rw = rho w_s (aligned instances) -- one multiply per draw instead of two.
+  static __device__ __forceinline__ void normals_w(Key key, uint32_t trial, uint32_t stream, uint32_t aux, int t, int S,
+                                                   R c, const R (&w)[NSLOT], C (&z)[NSLOT], R (&rw)[NSLOT]) {
+    static_assert(ALIGNED, "aligned slot map");
+    constexpr int Q = SL::HALF / 2;
+    const bool t0 = (t == 0);
+    const int qp = (S >> 2) - 1 + t;
+    auto draw = [&](int s, uint32_t w0, uint32_t w1) __attribute__((always_inline)) {
+      rw[s] = sqrt_n1(c * bm_log(w0, R(0))) * w[s];
+      R sn, cs;
+      sincos_lut(w1, sn, cs);
+      z[s] = mkc(rw[s] * cs, rw[s] * sn);
+    };
+#pragma unroll
+    for (int j = 0; j < Q; ++j) {
+      const bool sw = (j == 0) && t0;
+      uint4 u = philox4x32_10<kUni>(make_uint4(sw ? (uint32_t)((S >> 1) - 1) : (uint32_t)(qp + T * j), trial, stream, aux),
+                                    key);
+      draw(j, sw ? u.z : u.x, sw ? u.w : u.y);
+      draw(j + Q, sw ? u.x : u.z, sw ? u.y : u.w);
+      u = philox4x32_10<kUni>(make_uint4((uint32_t)(t + T * j), trial, stream, aux), key);
+      draw(SL::HALF + j, u.x, u.y);
+      draw(SL::HALF + j + Q, u.z, u.w);
+    }
+  }
+
   // |H|^2 of antenna a at the thread's slots for the closed-form channels (gen<false>'s
   // magnitudes, for pass 1's MRT norms): LoS |a1 e^{j phi1}|^2 = a1^2 -- no phase at all;
   // two-path |a1 e^{j phi1} - a2 e^{j phi2}|^2 = (a1 - a2)^2 + 4 a1 a2 sin^2((phi1 - phi2) / 2)
@@ -1037,6 +1064,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // laundering copy of 1 / ||Hhat||, 8 VALU per antenna: config 2 -0.2 %, MCNC -0.6 %, but the
   // CSI instance +5.3 % (its allocation again), so not with CSI (profiles/r05/ab/ab_*_wsc.json).
   constexpr bool WSC = PRE_EW && !CSI;
+  // ... and for the Rayleigh channel the weight is folded into the Box-Muller radius
+  // (CHN::normals_w): one multiply per draw instead of three, |h w|^2 from the radius
+#ifndef MIMO_WSC_RAY
+#define MIMO_WSC_RAY 1
+#endif
+  constexpr bool WSC_RAY = MIMO_WSC_RAY != 0 && WSC && CH == CH_RAYLEIGH && ALIGNED;  // (fp64: no pipelined draws)
   R wsc[WSC ? NSLOT : 1];
   auto array_pass = [&](bool main_pass, C (&acc)[NSLOT]) __attribute__((always_inline)) {
 #pragma unroll
@@ -1058,11 +1091,28 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       MIMO_ISA_MARK("array_pass");
       const int tl = opaque(tf);
       C h[NSLOT];
+      R rw[WSC_RAY ? NSLOT : 1];  // WSC_RAY: |h w| per slot
       if constexpr (PIPE) {
 #pragma unroll
         for (int s = 0; s < NSLOT; ++s) h[s] = hnext[s];
+      } else if constexpr (WSC_RAY) {
+        if (MIMO_ABL(p, ABL_RNG)) {  // ablation: the synthetic channel, scaled
+          CHN::template gen<FREL>(p, key, ch_trial, a, tl, rx, h);
+#pragma unroll
+          for (int s = 0; s < NSLOT; ++s) {
+            h[s] = cscale(h[s], wsc[s]);
+            rw[s] = sqrt_ieee(fmar(h[s].x, h[s].x, h[s].y * h[s].y));
+          }
+        } else {
+          const R sa = p.ant_rel[a];
+          CHN::normals_w(key, ch_trial, ST_CHAN, (uint32_t)a, tl, S, bm_c<R>(sa * sa), wsc, h, rw);
+        }
       } else {
         CHN::template gen<FREL>(p, key, ch_trial, a, tl, rx, h);
+        if constexpr (WSC) {
+#pragma unroll
+          for (int s = 0; s < NSLOT; ++s) h[s] = cscale(h[s], wsc[s]);
+        }
       }
       const int an = a + 1 < A ? a + 1 : a;
       const R san = PIPE ? p.ant_rel[an] : R(0);
@@ -1100,6 +1150,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       auto hest = [&](int s) __attribute__((always_inline)) -> C {
         if constexpr (CSI) return he[s]; else return h[s];
       };
+      // vk_part / alpha_s buffer: with ALPHA1 one (the designated wave reads vk_part(a) and
+      // every wave alpha(a) before the next antenna's IFFT barrier, which the next writes
+      // follow): compile-time LDS addresses; otherwise every wave reads vk_part(a) after the
+      // forward FFT, racing the next antenna's writes -- two buffers
+      const int vkb = ALPHA1 ? 0 : (a & 1);
       C x[NSLOT];
       R e2[NSLOT];  // |Hhat|^2, kept for g after the FFT
       R vk = R(0);
@@ -1110,17 +1165,17 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
           // the lattice point times conj(Hhat w), w = 1 / ||Hhat|| / sqrt(F): vk accumulates
           // |Hhat w|^2 = |Hhat|^2 / ||Hhat||^2 / F directly (11 f64 ops per slot, not 13;
           // vk_scale restores the factor F)
-          R in;
+          C ew;
           if constexpr (WSC) {
-            in = wsc[s];
+            ew = e;  // the loops carry h w already
           } else {
-            in = inv_nrm[s];
+            R in = inv_nrm[s];
             asm volatile("" : "+v"(in));
-            in *= inv_sqrt_f;
+            ew = cscale(e, in * inv_sqrt_f);
           }
-          const C ew = cscale(e, in);
           x[s] = cmulc(slab_point(s), ew);
-          vk = fmar(ew.x, ew.x, fmar(ew.y, ew.y, vk));
+          if constexpr (WSC_RAY) vk = fmar(rw[s], rw[s], vk);
+          else vk = fmar(ew.x, ew.x, fmar(ew.y, ew.y, vk));
           if constexpr (!E2_RE) e2[s] = fmar(e.x, e.x, e.y * e.y);
         } else {
           x[s] = cmulc(symw(s), e);  // s conj(Hhat) / ||Hhat|| / sqrt(F); 0 off band (symw = 0)
@@ -1130,18 +1185,21 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       }
       if (main_pass) {
         vk = wave_sum_lane63(vk);
-        if (lane == 63) vk_part[a & 1][wid] = vk;  // read after the IFFT's first barrier
+        if (lane == 63) vk_part[vkb][wid] = vk;  // read after the IFFT's first barrier
       }
       SL::scatter(d, x, t0);
+      // the FFTs take the thread id already laundered for this antenna (tl) where it is the
+      // physical one: their own opaque copy of it then costs no register move in run_second
+      const int tfft = SPLITFFT ? t : tl;
       if (!MIMO_ABL(p, ABL_FFT))
-        FFT::template run<+1, 0, SL::zero_mask()>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_ifft,
+        FFT::template run<+1, 0, SL::zero_mask()>(d, lds, WAVEFFT ? p.tw_wave : p.tw, tfft, MIMO_ABL(p, ABL_XCHG), hfill_ifft,
                                                   tw1);
       if (!MIMO_ABL(p, ABL_PA)) pa_block<COLD_OUT>(p.pa_kind, d, p.sat_tx, p.sqrt_sat_tx, p.inv_sat_tx, p.rapp_p, p.toi_tx);
       // alpha_a (Bussgang gain of antenna a's PA from its precoding power, main pass only)
       auto alpha_of_vk = [&]() __attribute__((always_inline)) -> R {
-        R vks = vk_part[a & 1][0];
+        R vks = vk_part[vkb][0];
 #pragma unroll
-        for (int i = 1; i < W; ++i) vks += vk_part[a & 1][i];
+        for (int i = 1; i < W; ++i) vks += vk_part[vkb][i];
         const R x = fmar(vks, PRE_EW ? p.inv_vk0_f : p.inv_vk0, -R(1));
         // Polynomial alpha: -7 % at F = 2048, but +3 % at F = 8192 (SGPR pressure of the
         // 8 waves/team instance, tools/ab_libs.py), so only up to F = 4096.
@@ -1175,13 +1233,15 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       // orders the hand-off (alpha_s double-buffered like vk_part).  The other waves skip the
       // partial sum and the 18-FMA polynomial.
       if constexpr (ALPHA1) {
+        // (ablation builds without the transforms' barriers: order the vk_part hand-off)
+        if (MIMO_ABL(p, ABL_FFT) || MIMO_ABL(p, ABL_XCHG)) __syncthreads();
         if (main_pass && wid == (a & (W - 1))) {
           const R al = alpha_of_vk();
-          if (lane == 0) alpha_s[a & 1] = al;
+          if (lane == 0) alpha_s[vkb] = al;
         }
       }
       if (!MIMO_ABL(p, ABL_FFT))
-        FFT::template run_second<-1>(d, lds, WAVEFFT ? p.tw_wave : p.tw, t, MIMO_ABL(p, ABL_XCHG), hfill_fft, tw1);
+        FFT::template run_second<-1>(d, lds, WAVEFFT ? p.tw_wave : p.tw, tfft, MIMO_ABL(p, ABL_XCHG), hfill_fft, tw1);
       if constexpr (PIPE) {
         if (MIMO_ABL(p, ABL_FFT)) {  // no transforms ran, so no exchange windows (ABL_XCHG keeps them)
 #pragma unroll
@@ -1191,7 +1251,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       // keep the vk_part / alpha_s hand-offs ordered when the ablations drop the barriers
       if (MIMO_ABL(p, ABL_FFT) || (ALPHA1 && MIMO_ABL(p, ABL_XCHG))) __syncthreads();
       R alpha_a = R(0);
-      if (main_pass) alpha_a = ALPHA1 ? alpha_s[a & 1] : alpha_of_vk();
+      if (main_pass) alpha_a = ALPHA1 ? alpha_s[vkb] : alpha_of_vk();
 #pragma unroll
       for (int s = 0; s < NSLOT; ++s) {
         const C y = SL::gather(d, s, t0);
@@ -1210,7 +1270,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       }
     }
 #pragma unroll
-    for (int s = 0; s < NSLOT; ++s) acc[s] = cscale(acc[s], inv_sqrt_f);
+    for (int s = 0; s < NSLOT; ++s) {
+      // WSC: sum_a (h w) y = w sum_a h y
+      if constexpr (WSC) acc[s] = cscale(acc[s], wsc[s] > R(0) ? inv_sqrt_f / wsc[s] : R(0));
+      else acc[s] = cscale(acc[s], inv_sqrt_f);
+    }
   };
 
   {
@@ -1228,7 +1292,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
     for (int s = 0; s < NSLOT; ++s) inv_nrm[s] = wsc[s] / inv_sqrt_f;
   }
 #pragma unroll
-  for (int s = 0; s < NSLOT; ++s) g[s] *= inv_nrm[s];
+  for (int s = 0; s < NSLOT; ++s) {
+    // WSC: g accumulated alpha |h w|^2 = w^2 alpha |h|^2, and inv_nrm / w^2 = 1 / (w / sqrt(F))
+    if constexpr (WSC) g[s] = wsc[s] > R(0) ? g[s] / (wsc[s] * inv_sqrt_f) : R(0);
+    else g[s] *= inv_nrm[s];
+  }
   uint32_t lab[NSLOT];
   gen_labels(opaque(tf), lab);
 

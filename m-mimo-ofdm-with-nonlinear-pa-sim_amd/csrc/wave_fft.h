@@ -169,20 +169,26 @@ struct WaveFft {
     const int w = tl >> 6, l = tl & 63;
     Sub::template run<DIR, 0, 0u>(d, lds + w * ROW, twl, l, no_xchg, fill, tw1);
     // B'[w, q] = B[w, q] e^{-j 2pi w q / F}, q = l + 64 m (wave-uniform branch)
-    // (all P loads issued before the first multiply: one wait instead of P round trips)
+    // (all P loads issued before the first multiply: one wait instead of P round trips).
+    // The products go straight to the exchange row inside the branch: merged back into d
+    // after it, they cost P register-pair copies per transform (v_mov_b64 at the join).
+    C* wb = lds + w * ROW + l;
     if (w > 0) {
       C tw[P];
 #pragma unroll
       for (int m = 0; m < P; ++m) tw[m] = Sub::gload(twl + TW_INTER, w * (l + 64 * m));
+      if (no_xchg) {
 #pragma unroll
-      for (int m = 0; m < P; ++m) d[m] = cmul(d[m], tw[m]);
-    }
-    if (!no_xchg) {
-      C* wb = lds + w * ROW + l;
+        for (int m = 0; m < P; ++m) d[m] = cmul(d[m], tw[m]);
+      } else {
+#pragma unroll
+        for (int m = 0; m < P; ++m) wb[64 * m] = cmul(d[m], tw[m]);
+      }
+    } else if (!no_xchg) {
 #pragma unroll
       for (int m = 0; m < P; ++m) wb[64 * m] = d[m];
-      __syncthreads();
     }
+    if (!no_xchg) __syncthreads();
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       C v[WV];
