@@ -16,12 +16,22 @@ the same on every box.  Groups:
   but a scatter of 1.1-2.8 x the stated rule's prediction (n_eff 750-2100 trials against
   its 2,442; the same per-point excess as the config-4 grids): mean z^2 <= 3,
   >= 75 % within 2 sigma.
+* CSI1_BIAS -- the step-1 CSI runs (family csi1: other revisions of the CSI drivers) with CNC
+  over LoS (eps 0 .. 0.7) and Rayleigh (eps 0.01 .. 0.2), and MCNC over Rayleigh: no bias
+  (median |rel| <= 0.5 %, every counter row's mean relative difference within +-2 %), but
+  their scatter exceeds the assumed stopping rule's (n_eff 200-1170 trials against its
+  2,442 -- those revisions' bits_sent_max is not known), so only loose z bounds.  The MCNC
+  LoS step-1 runs scatter exactly as the rule predicts (n_eff within 0.6-1.7 x n_ref) and
+  are in FIT.
 * Not compared (with their z maps): the 4-antenna curves (the shape differs,
   not only the level: a different configuration than the committed driver states), the
   1-antenna Rayleigh curves (the reference's workers replay one seeded channel sequence,
   channel.py:209-212 -- at one antenna that sample dominates: n_eff ~ n_ref / 10, a
   shared +1.3 % shift), and CNC two-path at 64 antennas (+1.9 % above IBO 5 dB where
-  the MCNC file of the same configuration agrees to 0.4 %).
+  the MCNC file of the same configuration agrees to 0.4 %), and the CNC LoS eps 0.18 file:
+  not an eps-0.18 run of this configuration -- its published no-distortion row lies below
+  the eps 0.10 file's and its iteration-8 row below the eps 0 file's
+  (tests/test_published_data.py).
 
 Noiseless runs: where the reference published BER 0 (no erroneous symbol in its trials),
 the engine's fraction q of erroneous trials must make that likely, (1 - q)^n_ref >= 1e-3;
@@ -39,7 +49,7 @@ import published_families as pf  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 NOT_COMPARED = {"ibo_cnc_two_path_nant64_ebn0_15", "small_cnc_rayleigh_nant1_ebn0_15",
-                "small_mcnc_rayleigh_nant1_ebn0_15"}
+                "small_mcnc_rayleigh_nant1_ebn0_15", "csi1_cnc_los_nant64_eps0.18"}
 
 
 def _group(c):
@@ -48,6 +58,8 @@ def _group(c):
         return None
     if c["family"] == "csi" and c["receiver"] == "cnc":
         return "csi_cnc"
+    if c["family"] == "csi1" and (c["receiver"] == "cnc" or c["channel"] == "rayleigh"):
+        return "csi1_bias"
     return "fit"
 
 
@@ -67,6 +79,13 @@ def test_published_family_curve(c):
         assert out["mean_z2"] <= 1.8 and out["max_abs_z"] <= 4.5
         for row, mz in out["row_mean_z"].items():
             assert abs(mz) <= 2.0, (row, mz)
+    elif g == "csi1_bias":
+        assert out["median_abs_rel"] <= 0.005
+        assert out["mean_z2"] <= 12.0 and out["frac_abs_z_le2"] >= 0.5
+        for row, rel in out["row_mean_rel"].items():
+            assert abs(rel) <= 0.02, (row, rel)
+        for row, mz in out["row_mean_z"].items():
+            assert abs(mz) <= 3.0, (row, mz)
     else:
         assert out["mean_z2"] <= 3.0 and out["frac_abs_z_le2"] >= 0.75
         for row, rel in out["row_mean_rel"].items():

@@ -11,6 +11,11 @@ layout axis, no-distortion, standard RX, CNC / MCNC iterations 1..8):
   runs), LoS, 64 antennas; plus the Rayleigh / two-path curves at Eb/N0 15 (IBO 0..8.5).
   Driver main_mp_miso_cnc_ber_vs_ibo.py:41-58,105 (bits_sent_max 1e7, n_err_min 1e5) and
   main_mp_miso_mcnc_ber_vs_ibo.py (same settings).
+* ``csi1``  -- BER vs Eb/N0 (5..20 dB, 1 dB) with CSI error: the step-1 runs of the same
+  drivers, over LoS (eps 0 .. 0.7, the driver's commented-out extension of csi_epsylon_lst)
+  and over Rayleigh (eps 0.01 .. 0.2; chan_lst = [Rayleigh]) -- other revisions of the
+  committed drivers, whose stopping rule (3e7 bits, n_err_min 1e7 / 1e6) is assumed
+  unchanged.  The LoS eps 0 .. 0.4 curves are independent re-runs of the ``csi`` family's.
 * ``small`` -- BER vs IBO at 1 and 4 antennas (LoS, Rayleigh, two-path), Eb/N0 15.  The
   same driver with n_ant_arr = [1] / [4] (assumed: the committed driver lists [64]).
 
@@ -30,7 +35,7 @@ the reference saw no erroneous symbol in n_c trials.  With q the fraction of the
 trials that hold any bit error, that has probability (1 - q)^n_c; a point where that is
 below 1e-3 would be a mismatch.
 
-    python tools/published_families.py [--family csi|ibo|small|all] [--out file.json]
+    python tools/published_families.py [--family csi|csi1|ibo|small|all] [--out file.json]
 """
 from __future__ import annotations
 
@@ -61,6 +66,16 @@ def _curves():
             out.append(dict(family="csi", receiver=rx, channel="los", n_ant=64, axis="ebn0", ibo=0.0, eps=eps,
                             bits_max=3e7, n_err_min=n_err,
                             file="ber_vs_ebn0_%s_los_csi_eps%1.3f_nant64_ibo0_ebn0_min5_max20_step0.50_%s" % (rx, eps, TAIL)))
+    for rx, n_err, grid in (("cnc", 1e7, {"los": (0.0, 0.01, 0.1, 0.18, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7),
+                                          "rayleigh": (0.01, 0.1, 0.2)}),
+                            ("mcnc", 1e6, {"los": (0.0, 0.01, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7),
+                                           "rayleigh": (0.01, 0.1)})):
+        for ch, epss in grid.items():
+            for eps in epss:
+                out.append(dict(family="csi1", receiver=rx, channel=ch, n_ant=64, axis="ebn0", ibo=0.0, eps=eps,
+                                bits_max=3e7, n_err_min=n_err,
+                                file="ber_vs_ebn0_%s_%s_csi_eps%1.3f_nant64_ibo0_ebn0_min5_max20_step1.00_%s"
+                                % (rx, ch, eps, TAIL)))
     for rx in ("cnc", "mcnc"):
         for ebn0 in (15, 1000):
             out.append(dict(family="ibo", receiver=rx, channel="los", n_ant=64, axis="ibo", ebn0=float(ebn0), eps=None,
@@ -83,7 +98,10 @@ CURVES = _curves()
 
 
 def curve_name(c):
-    tag = "eps%.1f" % c["eps"] if c["family"] == "csi" else "ebn0_%g" % c["ebn0"]
+    if c["family"] == "csi1":
+        tag = "eps%.2f" % c["eps"]
+    else:
+        tag = "eps%.1f" % c["eps"] if c["family"] == "csi" else "ebn0_%g" % c["ebn0"]
     return "%s_%s_%s_nant%d_%s" % (c["family"], c["receiver"], c["channel"], c["n_ant"], tag)
 
 
@@ -106,7 +124,7 @@ ROW_MAPS = {"full": lambda r: list(range(r)), "prefix": lambda r: list(range(r))
 
 
 def layout(c):
-    if c["family"] == "csi":
+    if c["family"] in ("csi", "csi1"):
         return "full"
     return "prefix" if c["family"] == "ibo" and c["channel"] == "los" else "no_clean"
 
