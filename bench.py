@@ -362,7 +362,11 @@ def main():
     if "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
         torch.cuda.set_device(dev)
-        dist.init_process_group(backend)
+        # device_id binds the RCCL communicator to this rank's GPU (no guessing from the rank)
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=torch.device(f"cuda:{dev}"))
+        else:
+            dist.init_process_group(backend)
     wl = WORKLOADS[args.workload]
     eng = make_engine(dev, args.workload, args.precision)
     iters = [int(x) for x in args.iters.split(",")]

@@ -321,7 +321,7 @@ def main():
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     rng = lambda s: np.arange(*[float(x) for x in s.split(":")])  # noqa: E731
     ibo_arr, ebn0_arr = rng(args.ibo), rng(args.ebn0)
     iters = np.asarray([int(x) for x in args.iters.split(",")])
