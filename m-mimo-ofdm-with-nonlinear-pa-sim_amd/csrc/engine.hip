@@ -424,7 +424,9 @@ int ensure_device(mimo_engine* e) {
   std::vector<float2> tws[2] = {twiddles(mimo::team_size(F), to_f32), twiddles(mimo::alt_team_size(F), to_f32)};
   std::vector<double2> tw64 = twiddles(mimo::team_size64(F), to_f64);
   // split FFT (split_fft.h): the F/2-point sub-transform's table, its cot-tan region, then
-  // the radix-2 stage's (cos a, tan a), a = -2 pi n / F, n < F/2
+  // the radix-2 stage's (cos a, tan a), a = -2 pi n / F, n < F/2.  At n = F/4 the pair is
+  // (6.1e-17, -1.6e16): c t rounds to sin a, and the product form c (u.x - t u.y) keeps full
+  // precision there (tests/test_fft_split.py, near the quarter turn)
   if (mimo::split_fft_used(F, mimo::team_size64(F), true)) {
     const int T = mimo::team_size64(F), P = F / T;
     tw64 = twiddles_of(F / 2, T / 2, to_f64);

@@ -152,3 +152,18 @@ def test_round_trip_with_pointwise_step(clip):
     for m in range(P):
         got[tau + T * m] = Y[:, m]
     assert np.max(np.abs(got - want)) < 1e-10 * np.max(np.abs(want))
+
+
+def test_r2_twiddle_product_form_near_quarter_turn():
+    """The (cos a, tan a) form at a = -pi/2 (n = F/4: cos 6.1e-17, tan -1.6e16) and its
+    neighbours: c (u.x - t u.y) + j c (u.y + t u.x) equals e^{ja} u to a few ulp of |u|, in
+    both directions -- c t rounds to sin a, so the large tangent loses nothing."""
+    c, t = r2_table()
+    rng = np.random.default_rng(4)
+    for n in (F // 4 - 2, F // 4 - 1, F // 4, F // 4 + 1, F // 4 + 2, 0, H - 1):
+        for DIR in (-1, +1):
+            u = complex(rng.standard_normal(), rng.standard_normal())
+            zero = np.zeros(1, complex)
+            got = bfly_ct(DIR, zero, np.array([u]), c[n], t[n])[0][0]
+            want = np.exp(DIR * 2j * np.pi * n / F) * u
+            assert abs(got - want) <= 4e-16 * abs(u), (n, DIR, abs(got - want) / abs(u))
