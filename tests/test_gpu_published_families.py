@@ -1,6 +1,7 @@
-"""The engine against three more families of the reference's published BER curves
-(VERDICT r4 item 1): channel-estimation error (CSI eps), BER vs IBO including the noiseless
-Eb/N0 = 1000 dB runs, and single-antenna arrays.  tools/published_families.py holds the
+"""The engine against four more families of the reference's published BER curves
+(VERDICT r4 item 1): channel-estimation error (CSI eps; the step-1 runs over LoS and
+Rayleigh as a fourth family), BER vs IBO including the noiseless Eb/N0 = 1000 dB runs, and
+single-antenna arrays.  tools/published_families.py holds the
 machinery (each driver's own stopping rule -> sigma of the published value; the engine's
 per-trial spread -> its own sigma); profiles/r05/families/ the measured statistics and z maps.
 

@@ -1,4 +1,4 @@
-"""The engine against three more families of BER curves the reference publishes.
+"""The engine against four more families of BER curves the reference publishes.
 
 Families (CSV data files of figs/csv_results, copied to tests/golden as published_*.csv; row
 layout axis, no-distortion, standard RX, CNC / MCNC iterations 1..8):
