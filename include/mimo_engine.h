@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MIMO_ABI_VERSION 7
+#define MIMO_ABI_VERSION 8
 
 enum { MIMO_OK = 0, MIMO_EINVAL = -1, MIMO_EHIP = -2, MIMO_ENOKERNEL = -3, MIMO_ENOMEM = -4 };
 enum { MIMO_PA_NONE = 0, MIMO_PA_SOFTLIM = 1, MIMO_PA_RAPP = 2, MIMO_PA_TOI = 3 };
@@ -98,6 +98,11 @@ typedef struct mimo_point {
   double cnc_toi_coeff;     /* CNC PA cubic coefficient                               */
   double cnc_alpha;         /* CNC alpha (corrector.py:106-110)                      */
   double csi_eps;           /* CSI error epsilon; < 0 = perfect CSI                   */
+  double array_alpha;       /* 0: each antenna's Bussgang gain from its precoding power
+                               (Link, mp_model.py:315-317).  > 0: that gain for every antenna --
+                               the TOI drivers' measured alpha_estimate
+                               (main_miso_cnc_ber_vs_ebn0_toi.py:95-121,247-249).  Not with the
+                               float32 F = 8192 instance (MIMO_EINVAL).  (ABI 8) */
 } mimo_point;
 
 int32_t mimo_abi_version(void);

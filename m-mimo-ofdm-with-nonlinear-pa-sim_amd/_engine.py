@@ -48,7 +48,8 @@ class MimoPoint(ctypes.Structure):
     _fields_ = [("ibo_db", ctypes.c_double), ("snr_db", ctypes.c_double), ("avg_symbol_power", ctypes.c_double),
                 ("pa_kind", ctypes.c_int32), ("cnc_pa_kind", ctypes.c_int32), ("sat_pow", ctypes.c_double),
                 ("p_hardness", ctypes.c_double), ("toi_coeff", ctypes.c_double), ("cnc_sat_pow", ctypes.c_double),
-                ("cnc_toi_coeff", ctypes.c_double), ("cnc_alpha", ctypes.c_double), ("csi_eps", ctypes.c_double)]
+                ("cnc_toi_coeff", ctypes.c_double), ("cnc_alpha", ctypes.c_double), ("csi_eps", ctypes.c_double),
+                ("array_alpha", ctypes.c_double)]
 
 
 SYMBOLS = {
@@ -93,6 +94,9 @@ class EngineError(RuntimeError):
     pass
 
 
+ABI_VERSION = 8  # include/mimo_engine.h MIMO_ABI_VERSION
+
+
 def lib():
     """Load the HIP engine library; raises if it was not built (no CPU fallback)."""
     global _lib
@@ -104,6 +108,10 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        # the structures above are ABI 8's (mimo_point.array_alpha): a stale library would
+        # read past the fields it knows
+        if handle.mimo_abi_version() != ABI_VERSION:
+            raise EngineError(f"{LIB_PATH} is ABI {handle.mimo_abi_version()}, this module ABI {ABI_VERSION}: rebuild it")
         _lib = handle
     return _lib
 
@@ -163,13 +171,15 @@ class Engine:
 
     @staticmethod
     def make_point(ibo_db, snr_db, avg_symbol_power, pa_kind, sat_pow=0.0, p_hardness=0.0, toi_coeff=0.0,
-                   cnc_pa_kind=None, cnc_sat_pow=0.0, cnc_toi_coeff=0.0, cnc_alpha=1.0, csi_eps=None):
+                   cnc_pa_kind=None, cnc_sat_pow=0.0, cnc_toi_coeff=0.0, cnc_alpha=1.0, csi_eps=None,
+                   array_alpha=None):
         """A mimo_point from the per-point object state (Link.point_params() keys)."""
         return MimoPoint(ibo_db=float(ibo_db), snr_db=float(snr_db), avg_symbol_power=float(avg_symbol_power),
                          pa_kind=PA_KINDS[pa_kind], cnc_pa_kind=PA_KINDS[cnc_pa_kind or pa_kind],
                          sat_pow=float(sat_pow), p_hardness=float(p_hardness), toi_coeff=float(toi_coeff),
                          cnc_sat_pow=float(cnc_sat_pow), cnc_toi_coeff=float(cnc_toi_coeff),
-                         cnc_alpha=float(cnc_alpha), csi_eps=-1.0 if csi_eps is None else float(csi_eps))
+                         cnc_alpha=float(cnc_alpha), csi_eps=-1.0 if csi_eps is None else float(csi_eps),
+                         array_alpha=0.0 if array_alpha is None else float(array_alpha))
 
     def set_point(self, ibo_db, snr_db, avg_symbol_power, pa_kind, **kw):
         pt = self.make_point(ibo_db, snr_db, avg_symbol_power, pa_kind, **kw)

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -319,6 +320,11 @@ int validate_point(const mimo_engine* e, const mimo_point* pt) {
   if (!(pt->cnc_alpha != 0)) return fail(MIMO_EINVAL, "cnc_alpha must be non-zero");
   if (pt->csi_eps >= 1.0) return fail(MIMO_EINVAL, "csi_eps must be < 1");
   if (pt->csi_eps >= 0 && e->cfg.n_ant > mimo::kMaxCsiAnt) return fail(MIMO_EINVAL, "CSI error supports n_ant <= 512");
+  if (!(pt->array_alpha >= 0) || !std::isfinite(pt->array_alpha))
+    return fail(MIMO_EINVAL, "array_alpha must be finite and >= 0");
+  // the float32 F 8192 instance forms alpha by the library formula only (no polynomial to hold a constant)
+  if (pt->array_alpha > 0 && e->cfg.precision == MIMO_PREC_F32 && e->cfg.n_fft == 8192)
+    return fail(MIMO_EINVAL, "array_alpha needs float64 or n_fft <= 4096");
   return MIMO_OK;
 }
 
@@ -357,6 +363,13 @@ void fill_point(mimo_engine* e, const mimo_point& pt, uint64_t seed, uint64_t fi
     for (int i = 0; i < 9; ++i) p.apoly[i] = (R)af.apoly[i];
     p.alpha_xlim = (R)af.xlim;
     for (int k = 0; k < 19; ++k) p.amono64[k] = af.amono[k];
+  }
+  if (pt.array_alpha > 0) {
+    // one fixed gain for every antenna: the kernel's alpha polynomial made the constant over
+    // the whole range (the Horner sums then return it exactly)
+    for (int i = 0; i < 9; ++i) p.apoly[i] = i == 0 ? (R)pt.array_alpha : R(0);
+    for (int k = 0; k < 19; ++k) p.amono64[k] = k == 0 ? pt.array_alpha : 0.0;
+    p.alpha_xlim = std::numeric_limits<R>::max();
   }
   p.es_over_snr = (R)(pt.avg_symbol_power / std::pow(10.0, pt.snr_db / 10.0));
   p.csi_a = csi ? (R)std::sqrt(1.0 - pt.csi_eps * pt.csi_eps) : R(1);

@@ -217,8 +217,9 @@ def avg_precoding_gain(p) -> float:
     return float(np.average(np.abs(np.asarray(p)) ** 2))
 
 
-def agc(hs, p, ibo_db, n_sub_carr, n_ant):
-    """``Link.recalculate_agc`` (mp_model.py:290-329) for one trial.
+def agc(hs, p, ibo_db, n_sub_carr, n_ant, alpha_fixed=None):
+    """``Link.recalculate_agc`` (mp_model.py:290-329) for one trial.  ``alpha_fixed``: one
+    gain for every antenna instead, as the TOI drivers' AGC (main_miso_cnc_ber_vs_ebn0_toi.py:247-259).
 
     Returns dict with ``hk_vk`` (clean-run gain, [S]), ``hk_vk_noise`` (scalar),
     ``alpha_vec`` ([A]), ``ak_hk_vk`` ([S]), ``ak_hk_vk_noise`` (scalar).
@@ -227,7 +228,7 @@ def agc(hs, p, ibo_db, n_sub_carr, n_ant):
     hk_vk = np.multiply(hs, p)
     hk_vk_avg = np.sum(hk_vk, axis=0)
     ibo_vec = 10 * np.log10(10 ** (ibo_db / 10) * n_sub_carr / (vk_pow * n_ant))
-    ak = calc_alpha(ibo_vec)[:, None]
+    ak = calc_alpha(ibo_vec)[:, None] if alpha_fixed is None else np.full((hs.shape[0], 1), float(alpha_fixed))
     ak_hk_vk_avg = np.sum(ak * hk_vk, axis=0)
     return dict(hk_vk=hk_vk_avg, hk_vk_noise=float(np.mean(np.abs(hk_vk_avg) ** 2)),
                 alpha_vec=ak[:, 0], ak_hk_vk=ak_hk_vk_avg,

@@ -49,6 +49,10 @@ class SimConfig:
     tx_pos: np.ndarray | None = field(default=None, repr=False)
     table_h: np.ndarray | None = field(default=None, repr=False)  # [A, F] channel_mat_fd for "table"
     csi_seed: int | None = None    # "table" + CSI: key of the one shared estimate (None: the run seed)
+    # the TOI drivers' measured alpha_estimate (main_miso_cnc_ber_vs_ebn0_toi.py:95-134,247-249):
+    # every antenna's AGC gain and the CNC receiver's alpha; None: Link's (mp_model.py:315-317)
+    array_alpha: float | None = None
+    cnc_alpha: float | None = None
 
     def __post_init__(self):
         if self.tx_pos is None:
@@ -98,6 +102,8 @@ def point_params(cfg: SimConfig):
         out["cnc_sat"] = rm.sat_pow(cfg.ibo_db, avg_samp)
         out["cnc_alpha"] = float(rm.calc_alpha(cfg.ibo_db))
         out["cnc_coeff"] = 0.0
+    if cfg.cnc_alpha is not None:
+        out["cnc_alpha"] = float(cfg.cnc_alpha)
     return out
 
 
@@ -126,7 +132,7 @@ def run_trial(cfg: SimConfig, labels, z_chan, z_noise, loc_u=None, z_csi=None, i
     h_est = rm.csi_error(h, cfg.csi_eps, z_csi) if cfg.csi_eps is not None else h
     p = rm.mrt_precoding(h_est)
     gain = rm.avg_precoding_gain(p)
-    g = rm.agc(h_est, p, cfg.ibo_db, cfg.n_sc, cfg.n_ant)
+    g = rm.agc(h_est, p, cfg.ibo_db, cfg.n_sc, cfg.n_ant, cfg.array_alpha)
     counts = []
 
     def nerr(lab):

@@ -23,7 +23,7 @@ def engine_for(cfg: SimConfig, device=-1, precision=None):
         kw = dict(sat_pow=rm.sat_pow(cfg.ibo_db, avg))
     eng.point_kw = dict(ibo_db=cfg.ibo_db, snr_db=cfg.snr_db, avg_symbol_power=pp["es"], pa_kind=cfg.pa,
                         p_hardness=cfg.p_hardness, cnc_pa_kind=cfg.pa, cnc_sat_pow=pp["cnc_sat"],
-                        cnc_toi_coeff=pp["cnc_coeff"], cnc_alpha=pp["cnc_alpha"], csi_eps=cfg.csi_eps, **kw)
+                        cnc_toi_coeff=pp["cnc_coeff"], cnc_alpha=pp["cnc_alpha"], csi_eps=cfg.csi_eps, array_alpha=cfg.array_alpha, **kw)
     eng.set_point(**eng.point_kw)
     return eng
 

@@ -30,14 +30,14 @@ def test_library_exports_every_declared_symbol():
     lib = _engine.lib()
     missing = [n for n in declared_functions() if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.mimo_abi_version() == 7
+    assert lib.mimo_abi_version() == 8
 
 
 def test_build_entry_checks_the_header_abi():
     """__graft_entry__.build() compares the library's ABI with include/mimo_engine.h's
     MIMO_ABI_VERSION (a hard-coded number there went stale once: ABI 5 -> 6)."""
     import __graft_entry__ as g
-    assert g._header_abi_version() == _engine.lib().mimo_abi_version() == 7
+    assert g._header_abi_version() == _engine.lib().mimo_abi_version() == 8
 
 
 def _cfg(**kw):
@@ -90,6 +90,26 @@ def test_valid_engine_is_host_only_until_run():
     assert lib.mimo_engine_set_point(h, ctypes.byref(bad)) == -1  # MIMO_EINVAL
     assert "csi_eps" in lib.mimo_last_error().decode()
     lib.mimo_engine_destroy(h)
+
+
+def test_set_point_array_alpha_validation():
+    """mimo_point.array_alpha (ABI 8): 0 = per-antenna gains; > 0 accepted by the float64
+    instances and by float32 up to F 4096; negative / non-finite values and float32 F 8192
+    (no alpha polynomial in that instance) are MIMO_EINVAL -- all host-side, no HIP."""
+    lib = _engine.lib()
+    for prec, n_fft, alpha, ok in ((0, 512, 0.93, True), (1, 512, 0.93, True), (0, 8192, 0.93, True),
+                                   (1, 8192, 0.93, False), (1, 8192, 0.0, True), (0, 512, -0.5, False),
+                                   (0, 512, float("nan"), False), (0, 512, float("inf"), False)):
+        c, keep = _cfg(n_fft=n_fft, n_sub_carr=n_fft // 2, precision=prec)
+        h = lib.mimo_engine_create(ctypes.byref(c))
+        assert h
+        pt = _engine.Engine.make_point(3.0, 20.0, 10.0, "toi", toi_coeff=0.01, cnc_toi_coeff=0.01, cnc_alpha=0.9,
+                                       array_alpha=alpha)
+        rc = lib.mimo_engine_set_point(h, ctypes.byref(pt))
+        assert (rc == 0) == ok, (prec, n_fft, alpha, rc, lib.mimo_last_error())
+        if not ok:
+            assert "array_alpha" in lib.mimo_last_error().decode()
+        lib.mimo_engine_destroy(h)
 
 
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):

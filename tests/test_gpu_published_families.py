@@ -32,7 +32,12 @@ the same on every box.  Groups:
   the MCNC file of the same configuration agrees to 0.4 %), and the CNC LoS eps 0.18 file:
   not an eps-0.18 run of this configuration -- its published no-distortion row lies below
   the eps 0.10 file's and its iteration-8 row below the eps 0 file's
-  (tests/test_published_data.py).
+  (tests/test_published_data.py); and the TOI family (third-order PA, two-path, 1 / 4
+  antennas): its no-distortion row agrees exactly but the distorted rows do not follow the
+  stated TOI under distortion.py's coefficient -- at TOI 22.75 dB the published standard RX
+  floors at BER 0.059 (an SDR of ~15 dB, where the stated TOI gives ~42 dB) while the TOI 5
+  file is ~100x milder than TOI 5 gives: those runs used a PA setting the files do not state
+  (profiles/r05/families/toi.json).
 
 Noiseless runs: where the reference published BER 0 (no erroneous symbol in its trials),
 the engine's fraction q of erroneous trials must make that likely, (1 - q)^n_ref >= 1e-3;
@@ -55,7 +60,7 @@ NOT_COMPARED = {"ibo_cnc_two_path_nant64_ebn0_15", "small_cnc_rayleigh_nant1_ebn
 
 def _group(c):
     name = pf.curve_name(c)
-    if c["n_ant"] == 4 or name in NOT_COMPARED:
+    if c["n_ant"] == 4 or name in NOT_COMPARED or c["family"] == "toi":
         return None
     if c["family"] == "csi" and c["receiver"] == "cnc":
         return "csi_cnc"

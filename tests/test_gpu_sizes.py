@@ -157,3 +157,39 @@ def test_pa_paths_per_instance_vs_oracle(F, S, pa, p, prec):
     _, _, per = eng.run(515, 0, n, iters, True, per_trial=True)
     print("pa path", F, S, pa, p, eng.describe(), per.sum(0), ref.sum(0))
     assert_counts_equal(per, ref, f"{F}/{S}/{pa}/{p} {prec}")
+
+
+ARRAY_ALPHA = [
+    # F,    S,    pa,        receiver, prec
+    (2048, 1024, "toi", "cnc", "f64"),
+    (2048, 1024, "toi", "cnc", "f32"),
+    (4096, 2048, "toi", "cnc", "f64"),
+    (4096, 2048, "toi", "mcnc", "f64"),
+    (4096, 2048, "toi", "cnc", "f32"),
+    (8192, 4096, "toi", "cnc", "f64"),
+    (2048, 1024, "softlim", "cnc", "f64"),
+]
+
+
+@pytest.mark.parametrize("F,S,pa,receiver,prec", ARRAY_ALPHA)
+def test_fixed_array_alpha_vs_oracle(F, S, pa, receiver, prec):
+    """mimo_point.array_alpha (ABI 8): one Bussgang gain for every antenna's AGC term and the
+    CNC receiver's alpha, as the TOI drivers run them (main_miso_cnc_ber_vs_ebn0_toi.py:95-134,
+    247-259) -- the kernel's alpha polynomial held constant.  Two-path channel (the TOI
+    drivers'), per-trial counts EXACTLY equal to the oracle's with the same fixed gain."""
+    A, M = 4, 64
+    snr = float(sim.rm.ebn0_to_snr(14.0, S, S, M))
+    cfg = sim.SimConfig(A, S, F, M, pa=pa, ibo_db=8.0 if pa == "toi" else 2.0, snr_db=snr, channel="two_path",
+                        receiver=receiver, array_alpha=0.93, cnc_alpha=0.93)
+    iters = [0, 1, 2]
+    n = 4
+    ref = sim.run_trials(cfg, 777, np.arange(n), iters=iters, incl_clean=True, chunk=2)
+    eng = engine_for(cfg, precision=prec)
+    _, _, per = eng.run(777, 0, n, iters, True, per_trial=True)
+    print("fixed alpha", F, S, pa, receiver, prec, eng.describe(), per.sum(0), ref.sum(0))
+    assert_counts_equal(per, ref, f"{F}/{S}/{pa}/{receiver} fixed alpha {prec}")
+    # and it is not the per-antenna gain: the oracle without the override counts differently
+    cfg0 = sim.SimConfig(A, S, F, M, pa=pa, ibo_db=cfg.ibo_db, snr_db=snr, channel="two_path", receiver=receiver,
+                         cnc_alpha=0.93)
+    ref0 = sim.run_trials(cfg0, 777, np.arange(n), iters=iters, incl_clean=True, chunk=2)
+    assert (ref0 != ref).any()

@@ -16,6 +16,14 @@ layout axis, no-distortion, standard RX, CNC / MCNC iterations 1..8):
   and over Rayleigh (eps 0.01 .. 0.2; chan_lst = [Rayleigh]) -- other revisions of the
   committed drivers, whose stopping rule (3e7 bits, n_err_min 1e7 / 1e6) is assumed
   unchanged.  The LoS eps 0 .. 0.4 curves are independent re-runs of the ``csi`` family's.
+* ``toi``   -- BER vs Eb/N0 (5..20 dB, 1 dB) with the third-order PA (TOI 22.75 dB), two-path,
+  1 and 4 antennas, CNC and MCNC: main_miso_{cnc,mcnc}_ber_vs_ebn0_toi.py (not the mp Link: the
+  drivers inline the loop, 1e7 bits / 1e5 errors).  Their AGC and receivers use one measured
+  gain for every antenna, alpha_estimate = mean over 1e4 unprecoded symbols of
+  |mean_k(rx_k / clean_k)| (:95-121,247-249): restated by toi_alpha_estimate() and passed as
+  mimo_point.array_alpha / cnc_alpha; the array PA's cubic coefficient is set with the
+  precoding gain of an unprecoded array (update_distortion before any set_precoding_matrix,
+  antenna_array.py:328-360), i.e. for the modem's average sample power.
 * ``small`` -- BER vs IBO at 1 and 4 antennas (LoS, Rayleigh, two-path), Eb/N0 15.  The
   same driver with n_ant_arr = [1] / [4] (assumed: the committed driver lists [64]).
 
@@ -85,6 +93,11 @@ def _curves():
             out.append(dict(family="ibo", receiver=rx, channel=ch, n_ant=64, axis="ibo", ebn0=15.0, eps=None,
                             bits_max=1e7, n_err_min=1e5,
                             file="ber_vs_ibo_%s_%s_nant64_ebn0_15_ibo_min0_max8_step0.50_%s" % (rx, ch, TAIL)))
+    for rx, na, tag, toi in (("cnc", 1, 22, 22.75), ("cnc", 1, 5, 5.0), ("cnc", 4, 22, 22.75),
+                             ("mcnc", 1, 22, 22.75), ("mcnc", 4, 22, 22.75)):
+        out.append(dict(family="toi", receiver=rx, channel="two_path", n_ant=na, axis="ebn0", toi=toi, eps=None,
+                        bits_max=1e7, n_err_min=1e5,
+                        file="toi_ber_vs_ebn0_%s_two_path_nant%d_ibo%d_ebn0_min5_max20_step1.00_%s" % (rx, na, tag, TAIL)))
     for rx in ("cnc", "mcnc"):
         for ch in ("los", "rayleigh", "two_path"):
             for na in (1, 4):
@@ -100,6 +113,8 @@ CURVES = _curves()
 def curve_name(c):
     if c["family"] == "csi1":
         tag = "eps%.2f" % c["eps"]
+    elif c["family"] == "toi":
+        tag = "toi%g" % c["toi"]
     else:
         tag = "eps%.1f" % c["eps"] if c["family"] == "csi" else "ebn0_%g" % c["ebn0"]
     return "%s_%s_%s_nant%d_%s" % (c["family"], c["receiver"], c["channel"], c["n_ant"], tag)
@@ -124,9 +139,36 @@ ROW_MAPS = {"full": lambda r: list(range(r)), "prefix": lambda r: list(range(r))
 
 
 def layout(c):
-    if c["family"] in ("csi", "csi1"):
+    if c["family"] in ("csi", "csi1", "toi"):
         return "full"
     return "prefix" if c["family"] == "ibo" and c["channel"] == "los" else "no_clean"
+
+
+def toi_alpha_estimate(toi_db, n_sym=10000, seed=4321, chunk=500):
+    """The TOI drivers' alpha_estimate (main_miso_cnc_ber_vs_ebn0_toi.py:95-121), restated.
+    The array is not precoded yet, so every antenna sends the same PA output and
+    rx_k / clean_k = Y_k / X_k on every in-band bin whatever the channel: alpha = the mean over
+    n_sym symbols of |mean_k Y_k / X_k|, X = the symbol's QAM points, Y = FFT(PA(IFFT(X))),
+    the PA at the modem's average sample power (distortion.py:222-241)."""
+    import modulation
+    mod = modulation.OfdmQamModem(constel_size=M, n_fft=N_FFT, n_sub_carr=N_SC, cp_len=1)
+    coeff = 1.0 / 10 ** (toi_db / 10) / mod.avg_sample_power
+    k = np.arange(N_SC)
+    bins = np.where(k < N_SC // 2, N_FFT - N_SC // 2 + k, k - N_SC // 2 + 1)  # modulation.py:266-267
+    const = np.asarray(mod.constellation)
+    rng = np.random.default_rng(seed)
+    acc, done = 0.0, 0
+    while done < n_sym:
+        n = min(chunk, n_sym - done)
+        s = const[rng.integers(0, M, (n, N_SC))]
+        fd = np.zeros((n, N_FFT), complex)
+        fd[:, bins] = s
+        x = np.fft.ifft(fd, norm="ortho", axis=1)
+        y = x - coeff * x * np.abs(x) ** 2                      # _process_toi (distortion.py:202-211)
+        r = np.fft.fft(y, norm="ortho", axis=1)[:, bins] / s
+        acc += float(np.abs(r.mean(axis=1)).sum())
+        done += n
+    return acc / n_sym
 
 
 def points(c, axis):
@@ -134,6 +176,22 @@ def points(c, axis):
     set_snr as the drivers call them)."""
     from link_util import build_link
     from utilities import ebn0_to_snr
+    if c["family"] == "toi":
+        # the geometry / channel / receiver of a Link; the PA is a point parameter (the mp Link
+        # itself takes no TOI array: it reads impairment.ibo_db, mp_model.py:83)
+        link, mod = build_link(n_ant=c["n_ant"], n_sc=N_SC, n_fft=N_FFT, M=M, cp=128, ibo=0.0, chan="two_path",
+                               is_mcnc=c["receiver"] == "mcnc")
+        alpha = toi_alpha_estimate(c["toi"])
+        coeff = 1.0 / 10 ** (c["toi"] / 10) / mod.avg_sample_power  # unprecoded gain 1 (see the docstring)
+        pts = []
+        for v in axis:
+            link.set_snr(float(ebn0_to_snr(float(v), N_SC, N_SC, M)))
+            pp = link.point_params()
+            pp.update(pa_kind="toi", sat_pow=0.0, toi_coeff=coeff, cnc_pa_kind="toi", cnc_sat_pow=0.0,
+                      cnc_toi_coeff=coeff, cnc_alpha=alpha, array_alpha=alpha)
+            pts.append(pp)
+        c["alpha_estimate"] = alpha
+        return link, pts
     link, _ = build_link(n_ant=c["n_ant"], n_sc=N_SC, n_fft=N_FFT, M=M, cp=128, ibo=0.0, chan=c["channel"],
                          is_mcnc=c["receiver"] == "mcnc", csi=c["eps"])
     pts = []
@@ -225,6 +283,8 @@ def measure(c, n_tr=None, seed0=5150, f32_check=False):
     maps = [main] if R == len(ITERS) + 1 else [main] + [m for m in ("prefix", "no_clean", "skip_std") if m != main]
     out = dict(curve=curve_name(c), file=c["file"], n_tr=n_tr, points=n_pt, rows=R, layout=main,
                seconds=round(dt, 2))
+    if "alpha_estimate" in c:
+        out["alpha_estimate"] = round(c["alpha_estimate"], 6)
     arrays = None
     for name in maps:
         cols = ROW_MAPS[name](R)
