@@ -17,6 +17,12 @@ the same on every box.  Groups:
   but a scatter of 1.1-2.8 x the stated rule's prediction (n_eff 750-2100 trials against
   its 2,442; the same per-point excess as the config-4 grids): mean z^2 <= 3,
   >= 75 % within 2 sigma.
+* FIT also holds the BER-vs-Eb/N0 curves at IBO 1 (the committed drivers' own setting) and
+  IBO 0 (family ebn0: LoS, two-path, Rayleigh x CNC, MCNC) and 32 more BER-vs-IBO files
+  (family ibo2: Eb/N0 10-20 and 1000 dB, IBO -9..9 included; row layout read from the data,
+  published_families.layout).  FIT_LOWCOUNT: two ibo2 files at Eb/N0 18 whose z statistics fit
+  (mean z^2 ~1) but whose few-error points put the median |rel| at 3-4 %: the FIT z bounds with
+  a 5 % median.  The noiseless ibo2 files (IBO down to -9 dB) hold float32 to >= 99.7 %.
 * CSI1_BIAS -- the step-1 CSI runs (family csi1: other revisions of the CSI drivers) with CNC
   over LoS (eps 0 .. 0.7) and Rayleigh (eps 0.01 .. 0.2), and MCNC over Rayleigh: no bias
   (median |rel| <= 0.5 %, every counter row's mean relative difference within +-2 %), but
@@ -32,7 +38,9 @@ the same on every box.  Groups:
   the MCNC file of the same configuration agrees to 0.4 %), and the CNC LoS eps 0.18 file:
   not an eps-0.18 run of this configuration -- its published no-distortion row lies below
   the eps 0.10 file's and its iteration-8 row below the eps 0 file's
-  (tests/test_published_data.py); and the TOI family (third-order PA, two-path, 1 / 4
+  (tests/test_published_data.py); the CNC LoS BER-vs-IBO file over IBO 0..8 at Eb/N0 15
+  (+1.9 %, mean z^2 3.4, where the MCNC file of the same configuration fits at 0.39 -- the same
+  pattern as the CNC two-path IBO 0..8 file above); and the TOI family (third-order PA, two-path, 1 / 4
   antennas): its no-distortion row agrees exactly but the distorted rows do not follow the
   stated TOI under distortion.py's coefficient -- at TOI 22.75 dB the published standard RX
   floors at BER 0.059 (an SDR of ~15 dB, where the stated TOI gives ~42 dB) while the TOI 5
@@ -55,7 +63,9 @@ import published_families as pf  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 NOT_COMPARED = {"ibo_cnc_two_path_nant64_ebn0_15", "small_cnc_rayleigh_nant1_ebn0_15",
-                "small_mcnc_rayleigh_nant1_ebn0_15", "csi1_cnc_los_nant64_eps0.18"}
+                "small_mcnc_rayleigh_nant1_ebn0_15", "csi1_cnc_los_nant64_eps0.18",
+                "ibo2_cnc_los_nant64_ebn0_15_ibo0_8_0.5"}
+FIT_LOWCOUNT = {"ibo2_cnc_los_nant64_ebn0_18_ibo0_9_0.25", "ibo2_cnc_two_path_nant64_ebn0_18_ibo0_9_0.25"}
 
 
 def _group(c):
@@ -66,6 +76,8 @@ def _group(c):
         return "csi_cnc"
     if c["family"] == "csi1" and (c["receiver"] == "cnc" or c["channel"] == "rayleigh"):
         return "csi1_bias"
+    if name in FIT_LOWCOUNT:
+        return "fit_lowcount"
     return "fit"
 
 
@@ -79,8 +91,8 @@ def test_published_family_curve(c):
     print(pf.curve_name(c), {k: v for k, v in out.items() if k not in ("z_map", "file")})
     g = _group(c)
     assert out["compared"] >= 20
-    assert out["median_abs_rel"] <= 0.03
-    if g == "fit":
+    assert out["median_abs_rel"] <= (0.05 if g == "fit_lowcount" else 0.03)
+    if g in ("fit", "fit_lowcount"):
         assert out["frac_abs_z_le1"] >= 0.5 and out["frac_abs_z_le2"] >= 0.85
         assert out["mean_z2"] <= 1.8 and out["max_abs_z"] <= 4.5
         for row, mz in out["row_mean_z"].items():
@@ -100,7 +112,10 @@ def test_published_family_curve(c):
             assert abs(mz) <= 0.6, (row, mz)
     # zero region: published 0 must be likely under the engine's rate of erroneous trials
     assert out["min_p_zero"] >= 1e-3
-    if noiseless:
+    if noiseless and c["family"] == "ibo":
         assert out["zero_points"] >= 100
         assert out["f32_entry_agreement"] >= 0.999
+        assert out["f32_mean_z2"] <= 1.8
+    elif noiseless:  # ibo2: down to IBO -9 dB, where float32 flips a few more decisions
+        assert out["f32_entry_agreement"] >= 0.997
         assert out["f32_mean_z2"] <= 1.8

@@ -1,4 +1,4 @@
-"""The engine against four more families of BER curves the reference publishes.
+"""The engine against five more families of BER curves the reference publishes.
 
 Families (CSV data files of figs/csv_results, copied to tests/golden as published_*.csv; row
 layout axis, no-distortion, standard RX, CNC / MCNC iterations 1..8):
@@ -16,6 +16,14 @@ layout axis, no-distortion, standard RX, CNC / MCNC iterations 1..8):
   and over Rayleigh (eps 0.01 .. 0.2; chan_lst = [Rayleigh]) -- other revisions of the
   committed drivers, whose stopping rule (3e7 bits, n_err_min 1e7 / 1e6) is assumed
   unchanged.  The LoS eps 0 .. 0.4 curves are independent re-runs of the ``csi`` family's.
+* ``ebn0``  -- BER vs Eb/N0 at 64 antennas, LoS / two-path / Rayleigh, CNC and MCNC, at IBO 1 dB
+  (5..20 dB, 1 dB: the committed drivers' own setting, main_mp_miso_{cnc,mcnc}_ber_vs_ebn0.py:40-58,
+  ibo_arr [1, 3], 1e7 bits, n_err_min 1e6) and at IBO 0 dB (0.5-dB steps, another revision of
+  the same drivers, stopping rule assumed unchanged).  The IBO 3 curves are
+  tests/test_gpu_link.py's.
+* ``ibo2``  -- every other BER-vs-IBO file at 64 antennas: Eb/N0 10, 12, 15, 18, 20 and 1000 dB,
+  IBO -9..9 / 0..9 / -3..3 in 0.25-2 dB steps (revisions of main_mp_miso_{cnc,mcnc}_ber_vs_ibo.py,
+  stopping rule as the ``ibo`` family's; row layout as that family's, the 10-row files "full").
 * ``toi``   -- BER vs Eb/N0 (5..20 dB, 1 dB) with the third-order PA (TOI 22.75 dB), two-path,
   1 and 4 antennas, CNC and MCNC: main_miso_{cnc,mcnc}_ber_vs_ebn0_toi.py (not the mp Link: the
   drivers inline the loop, 1e7 bits / 1e5 errors).  Their AGC and receivers use one measured
@@ -43,7 +51,7 @@ the reference saw no erroneous symbol in n_c trials.  With q the fraction of the
 trials that hold any bit error, that has probability (1 - q)^n_c; a point where that is
 below 1e-3 would be a mismatch.
 
-    python tools/published_families.py [--family csi|csi1|ibo|small|all] [--out file.json]
+    python tools/published_families.py [--family csi|csi1|ebn0|toi|ibo|small|all] [--out file.json]
 """
 from __future__ import annotations
 
@@ -93,6 +101,27 @@ def _curves():
             out.append(dict(family="ibo", receiver=rx, channel=ch, n_ant=64, axis="ibo", ebn0=15.0, eps=None,
                             bits_max=1e7, n_err_min=1e5,
                             file="ber_vs_ibo_%s_%s_nant64_ebn0_15_ibo_min0_max8_step0.50_%s" % (rx, ch, TAIL)))
+    for ibo, step in ((1, "1.00"), (0, "0.50")):
+        for rx in ("cnc", "mcnc"):
+            for ch in ("los", "two_path", "rayleigh"):
+                out.append(dict(family="ebn0", receiver=rx, channel=ch, n_ant=64, axis="ebn0", ibo=float(ibo), eps=None,
+                                bits_max=1e7, n_err_min=1e6,
+                                file="ber_vs_ebn0_%s_%s_nant64_ibo%d_ebn0_min5_max20_step%s_%s" % (rx, ch, ibo, step, TAIL)))
+    import re
+    named = {o["file"] for o in out}
+    pat = re.compile(r"ber_vs_ibo_(cnc|mcnc)_(los|rayleigh|two_path)_nant64_ebn0_(\d+)_ibo_min(-?\d+)_max(\d+)_step([\d.]+)_"
+                     + TAIL + r"\.csv$")
+    ibo_named = {"ber_vs_ibo_%s_los_nant64_ebn0_%d_ibo_min0_max9_step0.50_%s" % (rx, e, TAIL)
+                 for rx in ("cnc", "mcnc") for e in (15, 1000)}
+    ibo_named |= {"ber_vs_ibo_%s_%s_nant64_ebn0_15_ibo_min0_max8_step0.50_%s" % (rx, ch, TAIL)
+                  for rx in ("cnc", "mcnc") for ch in ("rayleigh", "two_path")}
+    for f in sorted(os.listdir(GOLDEN)):
+        m = pat.match(f[len("published_"):]) if f.startswith("published_") else None
+        if not m or f[len("published_"):-4] in named | ibo_named:
+            continue
+        rx, ch, e, lo, hi, st = m.groups()
+        out.append(dict(family="ibo2", receiver=rx, channel=ch, n_ant=64, axis="ibo", ebn0=float(e), eps=None,
+                        bits_max=1e7, n_err_min=1e5, ibo_range=(int(lo), int(hi), float(st)), file=f[len("published_"):-4]))
     for rx, na, tag, toi in (("cnc", 1, 22, 22.75), ("cnc", 1, 5, 5.0), ("cnc", 4, 22, 22.75),
                              ("mcnc", 1, 22, 22.75), ("mcnc", 4, 22, 22.75)):
         out.append(dict(family="toi", receiver=rx, channel="two_path", n_ant=na, axis="ebn0", toi=toi, eps=None,
@@ -115,6 +144,11 @@ def curve_name(c):
         tag = "eps%.2f" % c["eps"]
     elif c["family"] == "toi":
         tag = "toi%g" % c["toi"]
+    elif c["family"] == "ebn0":
+        tag = "ibo%g" % c["ibo"]
+    elif c["family"] == "ibo2":
+        lo, hi, st = c["ibo_range"]
+        tag = "ebn0_%g_ibo%d_%d_%g" % (c["ebn0"], lo, hi, st)
     else:
         tag = "eps%.1f" % c["eps"] if c["family"] == "csi" else "ebn0_%g" % c["ebn0"]
     return "%s_%s_%s_nant%d_%s" % (c["family"], c["receiver"], c["channel"], c["n_ant"], tag)
@@ -138,9 +172,18 @@ ROW_MAPS = {"full": lambda r: list(range(r)), "prefix": lambda r: list(range(r))
             "no_clean": lambda r: list(range(1, r + 1)), "skip_std": lambda r: [0] + list(range(2, r + 1))}
 
 
-def layout(c):
-    if c["family"] in ("csi", "csi1", "toi"):
+def layout(c, axis=None, pub=None):
+    """Row layout of a published file.  Ten rows: [clean, standard RX, iterations 1..8].  Nine
+    rows: decided by the data -- a first row that falls with IBO (Spearman rho < -0.8) is the
+    standard RX ("no_clean"); a flat one is the no-distortion run ("prefix").  The rule
+    reproduces every layout the fits tell apart (the wrong layouts: mean z^2 1e2-1e8)."""
+    if c["family"] in ("csi", "csi1", "toi", "ebn0") or (pub is not None and pub.shape[0] == len(ITERS) + 1):
         return "full"
+    if c["family"] in ("ibo", "ibo2") and pub is not None:
+        from scipy.stats import spearmanr
+        r0 = pub[0]
+        rho = 0.0 if np.all(r0 == r0[0]) else float(spearmanr(axis, r0)[0])
+        return "no_clean" if rho < -0.8 else "prefix"
     return "prefix" if c["family"] == "ibo" and c["channel"] == "los" else "no_clean"
 
 
@@ -279,7 +322,7 @@ def measure(c, n_tr=None, seed0=5150, f32_check=False):
     ber = (err / bits).T                                    # [column, point]
     sd = (per.astype(np.float64) / BPS).std(axis=1, ddof=1).T
     q = (per > 0).mean(axis=1).T                            # fraction of trials holding any error
-    main = layout(c)
+    main = layout(c, axis, pub)
     maps = [main] if R == len(ITERS) + 1 else [main] + [m for m in ("prefix", "no_clean", "skip_std") if m != main]
     out = dict(curve=curve_name(c), file=c["file"], n_tr=n_tr, points=n_pt, rows=R, layout=main,
                seconds=round(dt, 2))
