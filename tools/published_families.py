@@ -1,4 +1,4 @@
-"""The engine against five more families of BER curves the reference publishes.
+"""The engine against six more families of BER curves the reference publishes.
 
 Families (CSV data files of figs/csv_results, copied to tests/golden as published_*.csv; row
 layout axis, no-distortion, standard RX, CNC / MCNC iterations 1..8):
@@ -24,6 +24,9 @@ layout axis, no-distortion, standard RX, CNC / MCNC iterations 1..8):
 * ``ibo2``  -- every other BER-vs-IBO file at 64 antennas: Eb/N0 10, 12, 15, 18, 20 and 1000 dB,
   IBO -9..9 / 0..9 / -3..3 in 0.25-2 dB steps (revisions of main_mp_miso_{cnc,mcnc}_ber_vs_ibo.py,
   stopping rule as the ``ibo`` family's; row layout as that family's, the 10-row files "full").
+* ``small2`` -- BER vs Eb/N0 at 1, 4 and 16 antennas (IBO 0, and 1 antenna at IBO 20 / 50):
+  the BER-vs-Eb/N0 drivers with other n_ant_arr / ibo_arr (stopping rule assumed as theirs;
+  rows [clean, standard RX, the file's iterations]).
 * ``toi``   -- BER vs Eb/N0 (5..20 dB, 1 dB) with the third-order PA (TOI 22.75 dB), two-path,
   1 and 4 antennas, CNC and MCNC: main_miso_{cnc,mcnc}_ber_vs_ebn0_toi.py (not the mp Link: the
   drivers inline the loop, 1e7 bits / 1e5 errors).  Their AGC and receivers use one measured
@@ -51,7 +54,7 @@ the reference saw no erroneous symbol in n_c trials.  With q the fraction of the
 trials that hold any bit error, that has probability (1 - q)^n_c; a point where that is
 below 1e-3 would be a mismatch.
 
-    python tools/published_families.py [--family csi|csi1|ebn0|toi|ibo|small|all] [--out file.json]
+    python tools/published_families.py [--family csi|csi1|ebn0|ibo2|small2|toi|ibo|small|all] [--out file.json]
 """
 from __future__ import annotations
 
@@ -122,6 +125,15 @@ def _curves():
         rx, ch, e, lo, hi, st = m.groups()
         out.append(dict(family="ibo2", receiver=rx, channel=ch, n_ant=64, axis="ibo", ebn0=float(e), eps=None,
                         bits_max=1e7, n_err_min=1e5, ibo_range=(int(lo), int(hi), float(st)), file=f[len("published_"):-4]))
+    pat2 = re.compile(r"ber_vs_ebn0_(cnc|mcnc)_(los|rayleigh|two_path)_nant(1|4|16)_ibo(\d+)_ebn0_min(\d+)_max(\d+)"
+                      r"_step([\d.]+)_niter([\d_]+)\.csv$")
+    for f in sorted(os.listdir(GOLDEN)):
+        m = pat2.match(f[len("published_"):]) if f.startswith("published_") else None
+        if not m:
+            continue
+        rx, ch, na, ibo, lo, hi, st, it = m.groups()
+        out.append(dict(family="small2", receiver=rx, channel=ch, n_ant=int(na), axis="ebn0", ibo=float(ibo), eps=None,
+                        bits_max=1e7, n_err_min=1e6, ebn0_range=(int(lo), int(hi), float(st)), file=f[len("published_"):-4]))
     for rx, na, tag, toi in (("cnc", 1, 22, 22.75), ("cnc", 1, 5, 5.0), ("cnc", 4, 22, 22.75),
                              ("mcnc", 1, 22, 22.75), ("mcnc", 4, 22, 22.75)):
         out.append(dict(family="toi", receiver=rx, channel="two_path", n_ant=na, axis="ebn0", toi=toi, eps=None,
@@ -146,6 +158,9 @@ def curve_name(c):
         tag = "toi%g" % c["toi"]
     elif c["family"] == "ebn0":
         tag = "ibo%g" % c["ibo"]
+    elif c["family"] == "small2":
+        lo, hi, st = c["ebn0_range"]
+        tag = "ibo%g_ebn0_%d_%d_%g" % (c["ibo"], lo, hi, st)
     elif c["family"] == "ibo2":
         lo, hi, st = c["ibo_range"]
         tag = "ebn0_%g_ibo%d_%d_%g" % (c["ebn0"], lo, hi, st)
@@ -177,7 +192,7 @@ def layout(c, axis=None, pub=None):
     rows: decided by the data -- a first row that falls with IBO (Spearman rho < -0.8) is the
     standard RX ("no_clean"); a flat one is the no-distortion run ("prefix").  The rule
     reproduces every layout the fits tell apart (the wrong layouts: mean z^2 1e2-1e8)."""
-    if c["family"] in ("csi", "csi1", "toi", "ebn0") or (pub is not None and pub.shape[0] == len(ITERS) + 1):
+    if c["family"] in ("csi", "csi1", "toi", "ebn0", "small2") or (pub is not None and pub.shape[0] == len(ITERS) + 1):
         return "full"
     if c["family"] in ("ibo", "ibo2") and pub is not None:
         from scipy.stats import spearmanr
