@@ -63,6 +63,30 @@ def test_fixed_ber_grid_vs_published(receiver, channel):
     assert abs(sp["lag1_point_z_along_ebn0"]) <= sp["lag1_bound"], sp
 
 
+@pytest.mark.parametrize("channel", ["los", "two_path"])
+def test_fixed_ber_grid_mcnc_los_two_path(channel):
+    """The two MCNC fixed-BER grids the reference also publishes (LoS, two-path; round 5):
+    the bounds above, except that an iteration column may carry a small signed shift -- MCNC
+    LoS iteration 1 at -0.31 z, MCNC two-path iterations 6-8 at +0.24 ... +0.30 z, i.e. at most
+    0.5 % relative -- and the two-path grid reaches BER 1e-2 at one (IBO, iteration) cell that
+    the published grid does not (profiles/r05/config4/)."""
+    import fixed_ber_check
+    out, ber, pub, z = fixed_ber_check.run(channel, "mcnc", "f64")
+    print(out)
+    assert out["points"] == 400 and out["compared"] > 1000
+    assert out["max_abs_bias_per_iteration"] <= 0.01
+    assert out["median_rel"] <= 0.02
+    assert out["frac_abs_z_le2"] >= 0.75 and out["p95_abs_z"] <= 3.5
+    assert out["mean_z2"] <= 3.0 and out["max_abs_z"] <= 8.0
+    assert out["replica_self_check"]["frac_abs_z_le2"] >= 0.9
+    r = out["req_ebn0_at_ber_1e2"]
+    assert r["finite_mismatch"] <= 1 and r["compared"] >= 70 and r["mean_abs_db"] <= 0.1
+    sp = out["spread"]
+    assert sp["within_point_corr"] >= 0.85 and sp["rows_outside"] == 0, sp
+    assert max(abs(c["mean_z"]) for c in sp["iterations"]) <= 0.35, sp
+    assert abs(sp["lag1_point_z_along_ebn0"]) <= sp["lag1_bound"], sp
+
+
 def test_fixed_ber_grid_baseline_extent():
     """BASELINE config 4 at its stated extent (Eb/N0 0..30 x IBO 0..7 dB, 0.5 dB steps =
     915 points, CNC 0..8) on one GPU: every counter of every point closed
