@@ -63,17 +63,23 @@ def test_fixed_ber_grid_vs_published(receiver, channel):
     assert abs(sp["lag1_point_z_along_ebn0"]) <= sp["lag1_bound"], sp
 
 
-@pytest.mark.parametrize("channel", ["los", "two_path"])
-def test_fixed_ber_grid_mcnc_los_two_path(channel):
-    """The two MCNC fixed-BER grids the reference also publishes (LoS, two-path; round 5):
-    the bounds above, except that an iteration column may carry a small signed shift -- MCNC
-    LoS iteration 1 at -0.31 z, MCNC two-path iterations 6-8 at +0.24 ... +0.30 z, i.e. at most
-    0.5 % relative -- and the two-path grid reaches BER 1e-2 at one (IBO, iteration) cell that
-    the published grid does not (profiles/r05/config4/)."""
+@pytest.mark.parametrize("receiver,channel,n_ant,ibo_step", [
+    ("mcnc", "los", 64, 0.5), ("mcnc", "two_path", 64, 0.5),
+    ("cnc", "los", 64, 0.25), ("cnc", "rayleigh", 64, 0.25), ("cnc", "two_path", 64, 0.25),
+    ("cnc", "los", 1, 0.5), ("cnc", "two_path", 1, 0.5), ("mcnc", "los", 1, 0.5), ("mcnc", "two_path", 1, 0.5)])
+def test_fixed_ber_grid_more_published(receiver, channel, n_ant, ibo_step):
+    """Nine more fixed-BER grids the reference publishes (round 5, profiles/r05/config4/): the
+    MCNC LoS / two-path paper grids, the CNC grids at 0.25-dB IBO steps (800 points) and the
+    1-antenna LoS / two-path grids.  The bounds above, except that an iteration column may
+    carry a small signed shift (|mean z| <= 0.35 instead of 3 / sqrt(n): MCNC LoS iteration 1
+    at -0.31 z, MCNC two-path iterations 6-8 at +0.24 ... +0.30 z, at most 0.5 % relative) and
+    the MCNC two-path grid reaches BER 1e-2 at one (IBO, iteration) cell the published grid
+    does not.  The 1-antenna Rayleigh grids are left out: their point z correlate along Eb/N0
+    (lag-1 0.70 / 0.81), the reference's one replayed channel sequence."""
     import fixed_ber_check
-    out, ber, pub, z = fixed_ber_check.run(channel, "mcnc", "f64")
+    out, ber, pub, z = fixed_ber_check.run(channel, receiver, "f64", n_ant=n_ant, ibo_step=ibo_step)
     print(out)
-    assert out["points"] == 400 and out["compared"] > 1000
+    assert out["points"] == int(round(8 / ibo_step)) * 25 and out["compared"] > 1000
     assert out["max_abs_bias_per_iteration"] <= 0.01
     assert out["median_rel"] <= 0.02
     assert out["frac_abs_z_le2"] >= 0.75 and out["p95_abs_z"] <= 3.5

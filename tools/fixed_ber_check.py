@@ -51,19 +51,21 @@ N_ANT, N_SC, N_FFT, M, CP = 64, 2048, 4096, 64, 128
 BITS_MAX, N_ERR_MIN = int(5e6), int(1e5)
 
 
-def published(channel, receiver):
+def published(channel, receiver, n_ant=N_ANT, ibo_step=0.5):
+    """The published grid: IBO 0..7 in ``ibo_step`` steps (0.5 for the four paper grids; the
+    0.25-step 64-antenna and the 1-antenna files are other runs of the same driver)."""
     import utilities
-    name = ("published_fixed_ber1.0e-02_%s_%s_nant64_ebn0_min10_max22_step0.50_ibo_min0_max7_step0.50_"
-            "niter1_2_3_4_5_6_7_8" % (receiver, channel))
+    name = ("published_fixed_ber1.0e-02_%s_%s_nant%d_ebn0_min10_max22_step0.50_ibo_min0_max7_step%.2f_"
+            "niter1_2_3_4_5_6_7_8" % (receiver, channel, n_ant, ibo_step))
     rows = utilities.read_from_csv(name, directory=GOLDEN)
     ibo = np.asarray(rows[0], dtype=np.float64)
     ber = np.asarray(rows[1:], dtype=np.float64).reshape(len(ibo), -1, len(ITERS))
     return ibo, ber
 
 
-def build_link(channel, receiver, precision):
+def build_link(channel, receiver, precision, n_ant=N_ANT):
     import sweep
-    return sweep.paper_link(channel, receiver, precision, n_ant=N_ANT, n_sc=N_SC, n_fft=N_FFT, qam=M, cp=CP,
+    return sweep.paper_link(channel, receiver, precision, n_ant=n_ant, n_sc=N_SC, n_fft=N_FFT, qam=M, cp=CP,
                             n_err_min=N_ERR_MIN, bits_sent_max=BITS_MAX)
 
 
@@ -78,10 +80,11 @@ def reference_trials(pub_ber, bits_per_sym, per_counter=False):
     return np.minimum(budget, np.ceil(need.max(axis=-1)))
 
 
-def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137):
+def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137, n_ant=N_ANT, ibo_step=0.5):
     import sweep
     from utilities import ebn0_to_snr
-    link = build_link(channel, receiver, precision)
+    IBO = np.arange(0.0, 8.0, ibo_step)  # noqa: N806 (the grid of this published file)
+    link = build_link(channel, receiver, precision, n_ant)
     bits_per_sym = N_SC * int(np.log2(M))
     link.engine().run(0, 0, 1, [0])  # engine / device set-up and code-object load outside the timed sweep
     t0 = time.perf_counter()
@@ -100,7 +103,7 @@ def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137)
             params.append(dict(link.point_params()))
     P = len(params)
     from mp_model import _seed64
-    pub_ibo, pub = published(channel, receiver)
+    pub_ibo, pub = published(channel, receiver, n_ant, ibo_step)
     assert np.allclose(pub_ibo, IBO) and pub.shape == ber.shape, (pub_ibo, pub.shape, ber.shape)
     n_ref = reference_trials(pub, bits_per_sym).astype(np.int64)          # [ibo, ebn0]
     seeds = [_seed64(sweep.point_seed(seed + 1 + r, p)) for r in range(reps) for p in range(P)]
@@ -127,7 +130,7 @@ def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137)
     dreq = np.abs(req_gpu[fin] - req_pub[fin])  # only where both are finite (no inf - inf)
     n_sym = int(trials.sum())
     spread = spread_stats(z, sel, pub)
-    out = dict(channel=channel, receiver=receiver, precision=precision, points=int(P), ofdm_symbols=n_sym,
+    out = dict(channel=channel, receiver=receiver, precision=precision, n_ant=n_ant, ibo_step=ibo_step, points=int(P), ofdm_symbols=n_sym,
                wall_s=round(wall, 3), symbols_per_s=round(n_sym / wall, 1), compared=int(sel.sum()),
                max_abs_z=round(float(np.abs(z).max()), 3), p95_abs_z=round(float(np.percentile(np.abs(z[sel]), 95)), 3),
                mean_z2=round(float((z[sel] ** 2).mean()), 3),
@@ -276,6 +279,8 @@ def main():
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--out", default=None)
     ap.add_argument("--grid", default="published", choices=["published", "baseline"])
+    ap.add_argument("--n-ant", type=int, default=N_ANT)
+    ap.add_argument("--ibo-step", type=float, default=0.5)
     a = ap.parse_args()
     if a.grid == "baseline":
         out, ber = run_baseline(a.channel, a.receiver, a.precision)
@@ -283,7 +288,7 @@ def main():
         if a.out:
             np.savez(a.out, ber=ber)
         return
-    out, ber, pub, z = run(a.channel, a.receiver, a.precision)
+    out, ber, pub, z = run(a.channel, a.receiver, a.precision, n_ant=a.n_ant, ibo_step=a.ibo_step)
     print(json.dumps(out), flush=True)
     if a.out:
         np.savez(a.out, ber=ber, pub=pub, z=z)
