@@ -52,6 +52,25 @@ def test_pa_models(units):
     np.testing.assert_allclose(distortion.ThirdOrderNonLin(12, 20.95).process(x), units["pa_toi_out"], rtol=1e-12)
 
 
+def test_calc_alpha_vs_published_measured_gains():
+    """The reference's measured per-antenna Bussgang gains (figs/csv_results/
+    alpha_vs_tx_power_per_ant64_ibo0.0.csv, main_misc_evals/main_alpha_vs_tx_pow_per_ant_eval.py:
+    64 antennas under MRT at IBO 0, 1e4 symbols, rows (per-antenna IBO, measured alpha) for
+    Rayleigh, two-path and LoS): the engine's alpha at each antenna's own IBO -- the
+    per-antenna AGC term of mp_model.py:315-317 -- lies within the measurement's scatter
+    (Rayleigh: 2.1e-4, the spread channel powers; LoS / two-path: 1.1e-5)."""
+    import os
+    import _engine
+    a = np.loadtxt(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                "published_alpha_vs_tx_power_per_ant64_ibo0.0.csv"), delimiter=",")
+    assert a.shape == (6, 64)
+    for c, tol in ((0, 3e-4), (1, 2e-5), (2, 2e-5)):
+        ibo, measured = a[2 * c], a[2 * c + 1]
+        d = _engine.calc_alpha(ibo) - measured
+        print("channel row", c, "max |diff|", np.abs(d).max(), "mean", d.mean())
+        assert np.abs(d).max() <= tol
+
+
 def test_calc_alpha_vs_reference_and_mpmath(units):
     """The float64 kernels' Bussgang gain outside the per-point fit (alpha_fit.h segment
     table, mimo_calc_alpha): the reference's own calc_alpha outputs (units.npz, NumPy /
