@@ -88,6 +88,16 @@ __device__ __forceinline__ double rcp_r(double x) { return 1.0 / x; }
 //   [512, 768): (cos, sin)(2 pi i / 256)
 constexpr int kLnTab = 512, kScTab = 256, kLut64 = kLnTab + kScTab;
 static __shared__ double2 lut64[kLut64];
+// Diagnostic builds only (-DMIMO_DIAG_LUT_SEQ, wrong results): the table index's low 4 bits
+// replaced by the lane's, so every ds_read_b128 lane group (16 lanes with distinct lane & 15,
+// MI355X_MICROARCH §LDS) reads 16 distinct bank quads -- the random-index reads' bank
+// conflicts removed, their count and addresses' dependence kept (the conflict attribution
+// of profiles/r06/lut/).
+#ifdef MIMO_DIAG_LUT_SEQ
+__device__ __forceinline__ uint32_t lut_idx(uint32_t i) { return (i & ~15u) | (threadIdx.x & 15u); }
+#else
+__device__ __forceinline__ uint32_t lut_idx(uint32_t i) { return i; }
+#endif
 
 // sin / cos of 2 pi w 2^-32 (w: a uint32 word, revolutions): i = nearest 256th,
 // phi = 2 pi (w - i 2^24) 2^-32 in [-pi/256, pi/256], series to phi^7 / phi^6 and the
@@ -109,7 +119,7 @@ __device__ __forceinline__ void sincos_lut(uint32_t w, double& sn, double& cs) {
   double pc = fma(z, -(h2 * h2 * h2) / 720, (h2 * h2) / 24);
   pc = fma(pc, z, -h2 / 2);
   const double c = fma(z, pc, 1.0);
-  const double2 cst = lut64[kLnTab + (i & 255u)];
+  const double2 cst = lut64[kLnTab + lut_idx(i & 255u)];
   sn = fma(cst.y, c, cst.x * s);
   cs = fma(cst.x, c, -(cst.y * s));
 }
@@ -127,7 +137,7 @@ __device__ __forceinline__ void sincos_rev_lut(double r, double& sn, double& cs)
   double pc = fma(z, -1.0 / 720, 1.0 / 24);
   pc = fma(pc, z, -0.5);
   const double c = fma(z, pc, 1.0);
-  const double2 cst = lut64[kLnTab + ((int)n & 255)];
+  const double2 cst = lut64[kLnTab + lut_idx((uint32_t)((int)n & 255))];
   sn = fma(cst.y, c, cst.x * s);
   cs = fma(cst.x, c, -(cst.y * s));
 }
@@ -145,7 +155,7 @@ __device__ __forceinline__ double ln_unit(double x) {
   const double m = __builtin_amdgcn_frexp_mant(x);
   const int e = __builtin_amdgcn_frexp_exp(x) + ESC;
   const uint32_t hi = (uint32_t)__double2hiint(x);
-  const double2 cl = lut64[(hi >> 11) & 511u];
+  const double2 cl = lut64[lut_idx((hi >> 11) & 511u)];
   const double t = fma(m, cl.x, -1.0);
   double q = -1.0 / 6;
   q = fma(q, t, 1.0 / 5);
