@@ -315,7 +315,10 @@ if __name__ == "__main__":
     run_link("mid_cnc", 16, 256, 512, 64, 16, "softlim", 3.0, 3.0, "rayleigh", 15.0, [0, 1, 2, 3, 4], 24, 2137)
     run_link("cfg2_cnc", 64, 1024, 2048, 64, 128, "softlim", 3.0, 3.0, "rayleigh", 15.0, [0, 1, 2, 3, 4], 8, 2137)
     run_link("rapp", 8, 128, 256, 16, 8, "rapp", 2.0, 3.0, "rayleigh", 12.0, [0, 1, 2], 24, 77)
-    run_link("small_mcnc", 8, 64, 128, 16, 4, "softlim", 1.0, 3.0, "rayleigh", 12.0, [0, 1, 2], 16, 99)
+    # a CNC run (no mcnc=True): written as link_small_mcnc.npz, renamed link_a8_cnc.npz in round 6
+    # (file name only; the data are as captured).  No Link-level capture has is_mcnc=True: MCNC
+    # is pinned by the reference at the receiver level (units.npz mcnc_bits, make_units above).
+    run_link("a8_cnc", 8, 64, 128, 16, 4, "softlim", 1.0, 3.0, "rayleigh", 12.0, [0, 1, 2], 16, 99)
     run_link("los_cnc", 8, 128, 256, 64, 8, "softlim", 3.0, 3.0, "los", 20.0, [0, 1, 2], 16, 5)
     run_link("twopath_cnc", 8, 128, 256, 64, 8, "softlim", 3.0, 3.0, "two_path", 20.0, [0, 1, 2], 16, 6)
     run_link("csi_cnc", 8, 128, 256, 16, 8, "softlim", 2.0, 3.0, "rayleigh", 12.0, [0, 1, 2], 16, 7, csi=0.3)

@@ -36,22 +36,15 @@ the same on every box.  Groups:
   2,442 -- those revisions' bits_sent_max is not known), so only loose z bounds.  The MCNC
   LoS step-1 runs scatter exactly as the rule predicts (n_eff within 0.6-1.7 x n_ref) and
   are in FIT.
-* Not compared (with their z maps): the 4-antenna curves (the shape differs,
-  not only the level: a different configuration than the committed driver states), the
-  1-antenna Rayleigh curves (the reference's workers replay one seeded channel sequence,
-  channel.py:209-212 -- at one antenna that sample dominates: n_eff ~ n_ref / 10, a
-  shared +1.3 % shift), and CNC two-path at 64 antennas (+1.9 % above IBO 5 dB where
-  the MCNC file of the same configuration agrees to 0.4 %), and the CNC LoS eps 0.18 file:
-  not an eps-0.18 run of this configuration -- its published no-distortion row lies below
-  the eps 0.10 file's and its iteration-8 row below the eps 0 file's
-  (tests/test_published_data.py); the CNC LoS BER-vs-IBO file over IBO 0..8 at Eb/N0 15
-  (+1.9 %, mean z^2 3.4, where the MCNC file of the same configuration fits at 0.39 -- the same
-  pattern as the CNC two-path IBO 0..8 file above); and the TOI family (third-order PA, two-path, 1 / 4
-  antennas): its no-distortion row agrees exactly but the distorted rows do not follow the
-  stated TOI under distortion.py's coefficient -- at TOI 22.75 dB the published standard RX
-  floors at BER 0.059 (an SDR of ~15 dB, where the stated TOI gives ~42 dB) while the TOI 5
-  file is ~100x milder than TOI 5 gives: those runs used a PA setting the files do not state
-  (profiles/r05/families/toi.json).
+* Not compared (the z maps in profiles/r05/families/).  Every exclusion but one
+  is backed by the published files alone, in tests/test_published_data.py (CPU): the CNC LoS /
+  two-path IBO 0..8 files (below every other run of the same quantities), the 4-antenna LoS /
+  two-path curves (outside the band of the agreeing 1- and 64-antenna curves), the TOI family
+  (distortion ordered against the stated TOIs), the 1-antenna Rayleigh curves (below the
+  independent-channel closed form: the replayed channel sequence), two-path IBO 20 (iterations
+  unequal to the standard RX where nothing clips), LoS IBO 50 (a clean row worse than
+  guessing), the 16-antenna pair (CNC and MCNC disagree on the standard RX) and CNC LoS eps 0.18
+  (out of order).  Parity unresolved: the 4-antenna Rayleigh curves (no band to test against).
 
 Noiseless runs: where the reference published BER 0 (no erroneous symbol in its trials),
 the engine's fraction q of erroneous trials must make that likely, (1 - q)^n_ref >= 1e-3;
