@@ -104,14 +104,21 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise EngineError(f"{LIB_PATH} not found: build it with __graft_entry__.build() (make -C csrc)")
         handle = ctypes.CDLL(LIB_PATH)
+        # the ABI first: the structures below are ABI 8's (mimo_point.array_alpha),
+        # and a stale library lacks the newer entry points -- binding them first would raise a
+        # bare AttributeError instead of this message
+        ver = getattr(handle, "mimo_abi_version", None)
+        if ver is None:
+            raise EngineError(f"{LIB_PATH} exports no mimo_abi_version (older than ABI 2): rebuild it")
+        ver.restype, ver.argtypes = ctypes.c_int32, []
+        if ver() != ABI_VERSION:
+            raise EngineError(f"{LIB_PATH} is ABI {ver()}, this module ABI {ABI_VERSION}: rebuild it")
         for name, (res, args) in SYMBOLS.items():
-            fn = getattr(handle, name)
+            fn = getattr(handle, name, None)
+            if fn is None:
+                raise EngineError(f"{LIB_PATH} (ABI {ABI_VERSION}) lacks {name}: rebuild it")
             fn.restype = res
             fn.argtypes = args
-        # the structures above are ABI 8's (mimo_point.array_alpha): a stale library would
-        # read past the fields it knows
-        if handle.mimo_abi_version() != ABI_VERSION:
-            raise EngineError(f"{LIB_PATH} is ABI {handle.mimo_abi_version()}, this module ABI {ABI_VERSION}: rebuild it")
         _lib = handle
     return _lib
 

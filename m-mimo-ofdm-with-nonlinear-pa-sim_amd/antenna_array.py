@@ -3,7 +3,8 @@
 ``transmit`` batches all antennas into one GPU call per stage (map, IFFT, PA, FFT)
 instead of the reference's per-antenna Python loop (antenna_array.py:127-132), which
 re-ran the QAM mapper once per antenna.  Single-user MRT precoding runs on the GPU.
-Multi-user MR / ZF precoding (antenna_array.py:188-305) is mirrored on the host.
+Multi-user MR / ZF precoding (antenna_array.py:188-305) is not built:
+set_precoding_matrix raises NotImplementedError for per-user channel lists.
 """
 from __future__ import annotations
 

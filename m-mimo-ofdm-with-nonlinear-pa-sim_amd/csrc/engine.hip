@@ -254,11 +254,12 @@ mimo::InstanceKey select_instance(const mimo_engine* e, bool csi) {
 }
 
 template <typename R>
-hipError_t launch(const mimo::InstanceKey& k, dim3 grid, hipStream_t st, const mimo::TrialParams<R>& p, bool* found) {
+hipError_t launch(const mimo::InstanceKey& k, dim3 grid, hipStream_t st, const mimo::TrialParams<R>& p, bool* found,
+                  hipFuncAttributes* attr = nullptr) {
   constexpr bool F64 = sizeof(R) == 8;
 #define MIMO_LAUNCH_F(FV)                                                                    \
-  if constexpr (F64) return mimo::launch_trial_F##FV##_f64(k, grid, st, p, found);           \
-  else return mimo::launch_trial_F##FV##_f32(k, grid, st, p, found);
+  if constexpr (F64) return mimo::launch_trial_F##FV##_f64(k, grid, st, p, found, attr);     \
+  else return mimo::launch_trial_F##FV##_f32(k, grid, st, p, found, attr);
 #ifdef MIMO_ONLY_F  // single-size diagnostic / A-B builds (Makefile targets ablation, variant)
   if (k.F == MIMO_ONLY_F) {
 #if MIMO_ONLY_F == 2048
@@ -622,6 +623,25 @@ int run_points(mimo_engine* e, int n_points, const mimo_point* pts, const uint64
   }
   const mimo::InstanceKey key = select_instance(e, csi);
   if (int rc = ensure_device(e)) return rc;
+  if (csi) {
+    // the CSI instances add n_ant reals of dynamic LDS (the per-antenna power table) to their
+    // static LDS: check the sum against the CU's LDS before launching (F 8192 holds
+    // ~157 KiB statically, so A = 512 (4 KiB) is the edge)
+    hipFuncAttributes fa{};
+    bool found = false;
+    hipError_t qe = key.f64 ? launch(key, dim3(0), e->stream, mimo::TrialParams<double>{}, &found, &fa)
+                            : launch(key, dim3(0), e->stream, mimo::TrialParams<float>{}, &found, &fa);
+    int lds_max = 0;
+    if (found && qe == hipSuccess &&
+        hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, e->device) == hipSuccess &&
+        lds_max > 0) {
+      const size_t need = fa.sharedSizeBytes + (size_t)c.n_ant * (key.f64 ? sizeof(double) : sizeof(float));
+      if (need > (size_t)lds_max)
+        return fail(MIMO_EINVAL, "CSI error at n_ant = " + std::to_string(c.n_ant) + " needs " + std::to_string(need) +
+                                     " B of LDS per team (static " + std::to_string(fa.sharedSizeBytes) +
+                                     " + the per-antenna table), the device has " + std::to_string(lds_max));
+    }
+  }
   if (!c.reroll_chan && (c.channel_kind == MIMO_CH_LOS || c.channel_kind == MIMO_CH_TWOPATH)) {
     // fixed RX: jitter span 0 around (x0, x0); only consistent when rx_y == rx_x
     // (table channels never use the RX position)

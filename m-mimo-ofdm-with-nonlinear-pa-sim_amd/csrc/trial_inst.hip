@@ -53,30 +53,35 @@ constexpr Profile profile_for(int T, bool aligned, int ch) {
   return Profile{2, 2, false};
 }
 
+// attr != null: no launch, the instance's attributes instead (its static LDS, which the
+// engine checks with the CSI table's dynamic LDS against the device limit before a launch)
 template <int T, int NSLOT, bool AL, int CH, bool CSI>
-hipError_t go(dim3 grid, hipStream_t st, const TrialParams<Real>& p) {
+hipError_t go(dim3 grid, hipStream_t st, const TrialParams<Real>& p, hipFuncAttributes* attr) {
   constexpr Profile pr = profile_for(T, AL, CH);
+  auto* kern = &trial_kernel<Real, kF, T, NSLOT, AL, CH, CSI, pr.minw, pr.nbuf, pr.symw_lds>;
+  if (attr) return hipFuncGetAttributes(attr, reinterpret_cast<const void*>(kern));
   // CSI: the per-antenna power table is dynamic LDS, A reals (trial_kernel pw_csi)
   const size_t dyn = CSI ? sizeof(Real) * (size_t)p.n_ant : 0;
-  hipLaunchKernelGGL((trial_kernel<Real, kF, T, NSLOT, AL, CH, CSI, pr.minw, pr.nbuf, pr.symw_lds>), grid, dim3(T),
-                     dyn, st, p);
+  hipLaunchKernelGGL(kern, grid, dim3(T), dyn, st, p);
   return hipGetLastError();
 }
 
 template <int T, int NSLOT, bool AL>
-hipError_t by_channel(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams<Real>& p, bool* found) {
+hipError_t by_channel(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams<Real>& p, bool* found,
+                      hipFuncAttributes* a) {
   *found = true;
   switch (k.ch) {
     case CH_RAYLEIGH:
-      return k.csi ? go<T, NSLOT, AL, CH_RAYLEIGH, true>(grid, st, p)
-                   : go<T, NSLOT, AL, CH_RAYLEIGH, false>(grid, st, p);
+      return k.csi ? go<T, NSLOT, AL, CH_RAYLEIGH, true>(grid, st, p, a)
+                   : go<T, NSLOT, AL, CH_RAYLEIGH, false>(grid, st, p, a);
     case CH_LOS:
-      return k.csi ? go<T, NSLOT, AL, CH_LOS, true>(grid, st, p) : go<T, NSLOT, AL, CH_LOS, false>(grid, st, p);
+      return k.csi ? go<T, NSLOT, AL, CH_LOS, true>(grid, st, p, a) : go<T, NSLOT, AL, CH_LOS, false>(grid, st, p, a);
     case CH_TWOPATH:
-      return k.csi ? go<T, NSLOT, AL, CH_TWOPATH, true>(grid, st, p)
-                   : go<T, NSLOT, AL, CH_TWOPATH, false>(grid, st, p);
+      return k.csi ? go<T, NSLOT, AL, CH_TWOPATH, true>(grid, st, p, a)
+                   : go<T, NSLOT, AL, CH_TWOPATH, false>(grid, st, p, a);
     case CH_TABLE:
-      return k.csi ? go<T, NSLOT, AL, CH_TABLE, true>(grid, st, p) : go<T, NSLOT, AL, CH_TABLE, false>(grid, st, p);
+      return k.csi ? go<T, NSLOT, AL, CH_TABLE, true>(grid, st, p, a)
+                   : go<T, NSLOT, AL, CH_TABLE, false>(grid, st, p, a);
     default:
       *found = false;
       return hipSuccess;
@@ -84,19 +89,20 @@ hipError_t by_channel(const InstanceKey& k, dim3 grid, hipStream_t st, const Tri
 }
 
 template <int T>
-hipError_t by_team(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams<Real>& p, bool* found) {
+hipError_t by_team(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams<Real>& p, bool* found,
+                   hipFuncAttributes* a) {
   constexpr int P = kF / T;
   if (k.aligned) {
     if constexpr (8 < P) {
-      if (k.nslot == 8) return by_channel<T, 8, true>(k, grid, st, p, found);
+      if (k.nslot == 8) return by_channel<T, 8, true>(k, grid, st, p, found, a);
     }
     if constexpr (4 < P) {
-      if (k.nslot == 4) return by_channel<T, 4, true>(k, grid, st, p, found);
+      if (k.nslot == 4) return by_channel<T, 4, true>(k, grid, st, p, found, a);
     }
     return hipSuccess;
   }
   if (k.nslot != P) return hipSuccess;
-  return by_channel<T, P, false>(k, grid, st, p, found);
+  return by_channel<T, P, false>(k, grid, st, p, found, a);
 }
 
 }  // namespace
@@ -106,15 +112,16 @@ hipError_t by_team(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialP
 #else
 #define MIMO_LAUNCH_NAME MIMO_CAT(MIMO_CAT(launch_trial_F, INST_F), _f32)
 #endif
-hipError_t MIMO_LAUNCH_NAME(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams<Real>& p, bool* found) {
+hipError_t MIMO_LAUNCH_NAME(const InstanceKey& k, dim3 grid, hipStream_t st, const TrialParams<Real>& p, bool* found,
+                            hipFuncAttributes* attr) {
   *found = false;
   if (k.F != kF || k.f64 != kF64) return hipSuccess;
   if constexpr (kF64) {
-    if (k.T == team_size64(kF)) return by_team<team_size64(kF)>(k, grid, st, p, found);
+    if (k.T == team_size64(kF)) return by_team<team_size64(kF)>(k, grid, st, p, found, attr);
   } else {
-    if (k.T == team_size(kF)) return by_team<team_size(kF)>(k, grid, st, p, found);
+    if (k.T == team_size(kF)) return by_team<team_size(kF)>(k, grid, st, p, found, attr);
     if constexpr (alt_team_size(kF) != team_size(kF)) {
-      if (k.T == alt_team_size(kF)) return by_team<alt_team_size(kF)>(k, grid, st, p, found);
+      if (k.T == alt_team_size(kF)) return by_team<alt_team_size(kF)>(k, grid, st, p, found, attr);
     }
   }
   return hipSuccess;

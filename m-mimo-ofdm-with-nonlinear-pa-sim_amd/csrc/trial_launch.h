@@ -31,11 +31,14 @@ struct InstanceKey {
   bool f64;  // arithmetic type of the instance (TrialParams<double>)
 };
 
+// attr != null: return the instance's attributes (static LDS ...) instead of launching it
 #define MIMO_DECLARE_LAUNCH(FV)                                                                           \
   hipError_t launch_trial_F##FV##_f32(const InstanceKey& k, dim3 grid, hipStream_t st,                    \
-                                      const TrialParams<float>& p, bool* found);                          \
+                                      const TrialParams<float>& p, bool* found,                           \
+                                      hipFuncAttributes* attr = nullptr);                                 \
   hipError_t launch_trial_F##FV##_f64(const InstanceKey& k, dim3 grid, hipStream_t st,                    \
-                                      const TrialParams<double>& p, bool* found);
+                                      const TrialParams<double>& p, bool* found,                          \
+                                      hipFuncAttributes* attr = nullptr);
 MIMO_DECLARE_LAUNCH(128)
 MIMO_DECLARE_LAUNCH(256)
 MIMO_DECLARE_LAUNCH(512)

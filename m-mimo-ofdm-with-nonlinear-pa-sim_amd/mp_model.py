@@ -178,21 +178,35 @@ class SlotHeartbeat:
     1 s) from a daemon thread while the block runs, so that one long launch -- the engine
     call releases the GIL -- still reads as progress to waiting workers (beats
     only before set-up and after each batch let a first batch longer than the stall time
-    trigger the waiters' escape)."""
+    trigger the waiters' escape).
 
-    def __init__(self, dev: int, period_s: float = None):
+    The beats are tied to bounded work: the thread beats only while the work
+    since the last ``progress()`` call -- engine set-up plus the first batch, then one batch --
+    is younger than ``max_work_s`` (MIMO_SLOT_MAX_LAUNCH_S, default 120 s; a 65,536-trial batch
+    of the largest array takes ~1 s).  A holder hung inside a launch or anywhere in its loop
+    then falls silent, and the waiters' stall escape (wait_for_device_slot) fires again."""
+
+    def __init__(self, dev: int, period_s: float = None, max_work_s: float = None):
         import threading
         self.dev = int(dev)
         self.period_s = float(os.environ.get("MIMO_SLOT_HEARTBEAT_S", "1.0")) if period_s is None else period_s
+        self.max_work_s = float(os.environ.get("MIMO_SLOT_MAX_LAUNCH_S", "120")) if max_work_s is None else max_work_s
+        self._t_work = time.monotonic()
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._run, daemon=True)
 
+    def progress(self):
+        """A unit of work (a batch) completed: beat now and restart the work clock."""
+        self._t_work = time.monotonic()
+        slot_heartbeat(self.dev)
+
     def _run(self):
         while not self._stop.wait(self.period_s):
-            slot_heartbeat(self.dev)
+            if time.monotonic() - self._t_work <= self.max_work_s:
+                slot_heartbeat(self.dev)
 
     def __enter__(self):
-        slot_heartbeat(self.dev)
+        self.progress()
         self._thread.start()
         return self
 
@@ -206,8 +220,10 @@ def slot_activity(dev: int) -> int:
     """Latest heartbeat (lock-file mtime, ns) of ``dev``'s slots; 0 if none.  Any holder's
     beat counts, including a holder busy with other counters (another grid point, another
     driver sharing the lock directory): a waiter then keeps waiting until such holders
-    finish their runs instead of creating an extra engine -- bounded by those runs, never a
-    deadlock, since a holder's slot is released when its process exits."""
+    finish their runs instead of creating an extra engine.  Bounded: a holder beats only
+    while its current batch is younger than MIMO_SLOT_MAX_LAUNCH_S (SlotHeartbeat), so a hung
+    holder falls silent and the waiter's stall escape fires; a holder's slot is released
+    when its process exits."""
     d = _slot_dir()
     cap = max(1, int(os.environ.get("MIMO_MAX_ENGINES_PER_DEVICE", "2")))
     latest = 0
@@ -377,12 +393,12 @@ class Link:
                 return
         else:
             acquire_device_slot(dev)  # private counters: nobody else closes them, never wait
-        with SlotHeartbeat(dev):
+        with SlotHeartbeat(dev) as beat:
             self._simulate_loop(incl_clean_run, reroll_chan, cnc_n_iter_lst, seed_arr, n_err_shared_arr,
-                                n_bits_sent_shared_arr, err_np)
+                                n_bits_sent_shared_arr, err_np, beat)
 
     def _simulate_loop(self, incl_clean_run, reroll_chan, cnc_n_iter_lst, seed_arr, n_err_shared_arr,
-                       n_bits_sent_shared_arr, err_np):
+                       n_bits_sent_shared_arr, err_np, beat=None):
         eng = self.engine(reroll_chan)
         seed = _seed64(seed_arr)
         iters_all = np.asarray(cnc_n_iter_lst, dtype=np.int64).reshape(-1)
@@ -405,6 +421,8 @@ class Link:
                            self.max_batch)
             uniq = sorted(set(run_iters))
             e, b, _ = eng.run(seed, trial, n, uniq, clean_on)
+            if beat is not None:
+                beat.progress()  # one batch done: the heartbeat's work clock restarts
             trial += n
             pos = {it: j + (1 if clean_on else 0) for j, it in enumerate(uniq)}
             lock = n_err_shared_arr.get_lock() if hasattr(n_err_shared_arr, "get_lock") else None

@@ -346,7 +346,9 @@ def main():
                     tag, ibo, min(ebn0_arr), max(ebn0_arr), ebn0_arr[1] - ebn0_arr[0],
                     "_".join(str(v) for v in iters[1:]))
                 save_to_csv(ber_vs_ebn0_rows(ebn0_arr, ber[i].T), name, directory=args.out)
-        n_sym = int(bits[..., 0].sum()) // (args.n_sc * int(np.log2(args.qam)))
+        # every counter of a point shares its trials; the one that stayed open longest saw them
+        # all (iteration 0 closes first in a fixed-BER grid): symbols from the largest counter
+        n_sym = int(bits.max(axis=-1).sum()) // (args.n_sc * int(np.log2(args.qam)))
         print(f"sweep done: {len(ibo_arr) * len(ebn0_arr)} points, {n_sym} OFDM symbols on {world} GPU(s) in "
               f"{elapsed:.1f} s -> {args.out}")
     if dist is not None:

@@ -17,6 +17,8 @@ def build_link(n_ant=8, n_sc=64, n_fft=128, M=16, cp=4, pa="softlim", ibo=1.0, p
         dist = distortion.SoftLimiter(0, mod.avg_sample_power)
     elif pa == "rapp":
         dist = distortion.Rapp(ibo_db=0, p_hardness=p_hard, avg_samp_pow=mod.avg_sample_power)
+    elif pa == "toi":
+        dist = distortion.ThirdOrderNonLin(toi_db=ibo, avg_samp_pow=mod.avg_sample_power)
     else:
         raise ValueError(pa)
     tx = transceiver.Transceiver(modem=copy.deepcopy(mod), impairment=copy.deepcopy(dist), center_freq=int(3.5e9),

@@ -180,3 +180,22 @@ def test_calc_alpha_validates_without_a_gpu():
     assert lib.mimo_calc_alpha(out.ctypes.data_as(dp), 0, out.ctypes.data_as(dp)) == 0
     assert lib.mimo_calc_alpha(out.ctypes.data_as(dp), -1, out.ctypes.data_as(dp)) == -1  # MIMO_EINVAL
     assert "n < 0" in lib.mimo_last_error().decode()
+
+
+def test_stale_library_reports_its_abi(tmp_path, monkeypatch):
+    """a library of an older ABI (here 6, without mimo_cnc_receive_ex) is reported
+    as such -- the version is checked before the newer entry points are bound, so the error
+    is the 'rebuild it' EngineError, not a bare AttributeError."""
+    import shutil
+    import subprocess
+    import _engine
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    src = tmp_path / "stale.c"
+    src.write_text("int mimo_abi_version(void) { return 6; }\n")
+    so = tmp_path / "libstale.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    monkeypatch.setattr(_engine, "_lib", None)
+    monkeypatch.setattr(_engine, "LIB_PATH", str(so))
+    with pytest.raises(_engine.EngineError, match="is ABI 6, this module ABI 8: rebuild it"):
+        _engine.lib()

@@ -193,3 +193,21 @@ def test_fixed_array_alpha_vs_oracle(F, S, pa, receiver, prec):
                          cnc_alpha=0.93)
     ref0 = sim.run_trials(cfg0, 777, np.arange(n), iters=iters, incl_clean=True, chunk=2)
     assert (ref0 != ref).any()
+
+
+@pytest.mark.parametrize("F,S,n", [(8192, 4096, 2), (4096, 2048, 3)])
+def test_csi_at_max_antennas_vs_oracle(F, S, n):
+    """CSI error at n_ant = kMaxCsiAnt (512), where the per-antenna power table is
+    4 KiB of dynamic LDS next to the instance's static LDS (the F 8192 split-FFT instance holds
+    ~157 KiB: the edge of the CU's 160 KiB; engine.hip checks the sum before launching).
+    float64, per-trial counts EXACTLY equal to the oracle's."""
+    M = 16
+    snr = float(sim.rm.ebn0_to_snr(10.0, S, S, M))
+    cfg = sim.SimConfig(512, S, F, M, pa="softlim", ibo_db=2.0, snr_db=snr, channel="rayleigh", receiver="cnc",
+                        csi_eps=0.2)
+    iters = [0, 1]
+    ref = sim.run_trials(cfg, 88, np.arange(n), iters=iters, incl_clean=True, chunk=1)
+    eng = engine_for(cfg, precision="f64")
+    _, _, per = eng.run(88, 0, n, iters, True, per_trial=True)
+    print("csi max ant", F, eng.describe(), per.sum(0), ref.sum(0))
+    assert_counts_equal(per, ref, f"CSI A=512 F={F} f64")

@@ -249,6 +249,12 @@ def _slow_holder(lock_dir, beat, hold_s, q):
         with mp_model.SlotHeartbeat(0, period_s=0.2):
             time.sleep(hold_s)
         return
+    if beat == "hung":
+        # a holder hung inside its loop -- the heartbeat thread runs, but no batch
+        # completes (no progress()) for longer than the work bound: it must fall silent
+        with mp_model.SlotHeartbeat(0, period_s=0.2, max_work_s=0.5):
+            time.sleep(hold_s)
+        return
     t0 = time.monotonic()
     while time.monotonic() - t0 < hold_s:
         if beat:
@@ -256,11 +262,13 @@ def _slow_holder(lock_dir, beat, hold_s, q):
         time.sleep(0.2)
 
 
-@pytest.mark.parametrize("beat", [True, False, "thread"])
+@pytest.mark.parametrize("beat", [True, False, "thread", "hung"])
 def test_slot_wait_counts_holder_heartbeats_as_progress(tmp_path, monkeypatch, beat):
     """a holder whose first batch outlasts the stall time still counts as working
     when it beats its slot's heartbeat: the waiter keeps waiting (no extra engine) and takes
-    the slot when the holder exits.  Without heartbeats the waiter gives up after stall_s."""
+    the slot when the holder exits.  Without heartbeats the waiter gives up after stall_s --
+    and so it does when the holder's heartbeat thread runs but its batch has not
+    completed within the work bound (a holder hung in a launch): the beats stop."""
     import time
     import warnings
     import mp_model
@@ -281,7 +289,10 @@ def test_slot_wait_counts_holder_heartbeats_as_progress(tmp_path, monkeypatch, b
     p.join(60)
     assert got is True
     gave_up = any("MIMO_MAX_ENGINES_PER_DEVICE" in str(x.message) for x in w)
-    if beat:
+    if beat == "hung":
+        # silent from 0.5 s on: the waiter escapes ~stall_s later, well before the holder exits
+        assert gave_up and waited < hold - 0.5, waited
+    elif beat:
         assert not gave_up and waited >= hold - 0.5, (waited, [str(x.message) for x in w])
         assert (os.getpid(), 0) in mp_model._SLOTS  # the freed slot is now this process's
     else:
@@ -330,3 +341,22 @@ def test_next_batch_rows_equals_next_batch():
         for i in range(P):
             if act[i].any():
                 assert got[i] == mp_model.next_batch(err[i], bits[i], act[i], nbps, nmin, bmax, 65536), (i, err[i], bits[i])
+
+
+def test_fixed_toi_array_alpha_is_an_engine_level_parameter():
+    """the TOI drivers' one-gain AGC (alpha_estimate, main_miso_cnc_ber_vs_ebn0_toi.py:
+    95-121,247-249) does not run through Link: those drivers inline their loop, and the
+    reference's Link cannot hold a TOI array at all -- it reads impairment.ibo_db
+    (mp_model.py:83), which ThirdOrderNonLin lacks; the mirror fails the same way.  The fixed
+    gain is therefore engine-level: the TOI path (tools/published_families.points, the drivers'
+    restatement) passes it as mimo_point.array_alpha on every point, and make_point carries it."""
+    import _engine
+    import published_families as pf
+    with pytest.raises(AttributeError, match="ibo_db"):
+        build_link(n_ant=4, pa="toi", ibo=22.75)
+    c = dict(next(c for c in pf.CURVES if c["family"] == "toi" and c["n_ant"] == 1 and c["toi"] == 22.75))
+    _, pts = pf.points(c, np.array([10.0, 15.0]))
+    assert 0.98 < c["alpha_estimate"] < 1.0
+    for pp in pts:
+        assert pp["pa_kind"] == "toi" and pp["array_alpha"] == c["alpha_estimate"] == pp["cnc_alpha"]
+        assert _engine.Engine.make_point(**pp).array_alpha == c["alpha_estimate"]

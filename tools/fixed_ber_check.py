@@ -90,7 +90,9 @@ def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137,
     t0 = time.perf_counter()
     err, bits = sweep.run_grid(link, IBO, EBN0, ITERS, incl_clean=False, seed=seed)
     wall = time.perf_counter() - t0
-    trials = bits[..., 0] / bits_per_sym
+    # a point's trials: its counters share them, and the one open longest saw them all (iteration
+    # 0 closes first in a fixed-BER grid), so the largest counter, not counter 0
+    trials = bits.max(axis=-1) / bits_per_sym
     trials_c = bits / bits_per_sym            # per counter: a closed counter stops accumulating
     ber = err / bits
     # replicas of the reference's estimator at its trial counts (independent seeds)
@@ -240,7 +242,7 @@ def run_baseline(channel="rayleigh", receiver="cnc", precision="f64", seed=2137)
     err, bits = sweep.run_grid(link, BASE_IBO, BASE_EBN0, ITERS, incl_clean=False, seed=seed)
     wall = time.perf_counter() - t0
     ber = err / bits
-    trials = bits[..., 0] / bits_per_sym
+    trials = bits.max(axis=-1) / bits_per_sym  # a point's trials (its longest-open counter)
     closed = (err >= N_ERR_MIN) | (bits >= BITS_MAX)
     # standard receiver (iteration 0): BER(Eb/N0) non-increasing per IBO, beyond 4 sigma of
     # binomial noise at the measured counts (bits within a symbol are correlated: x 8 margin)
