@@ -414,10 +414,11 @@ __device__ __forceinline__ void sincos_phase(double r, double& sn, double& cs) {
   sincos_rev_lut(r, sn, cs);
 }
 
-template <typename R, int F, int T, int NSLOT, bool ALIGNED, int CH>
+template <typename R, int F, int T, int NSLOT, bool ALIGNED, int CH, bool UNI_EXTRA = false>
 struct Channel {
-  // philox.h UNI rounds: the fp64 wave-split instances (F <= 2048) only
-  static constexpr bool kUni = sizeof(R) == 8 && wave_fft_used(F, T, true);
+  // philox.h UNI rounds (the rounds whose words are uniform across the team on the SALU): the
+  // fp64 wave-split instances (F <= 2048), and UNI_EXTRA (the F 4096 CSI instance, below)
+  static constexpr bool kUni = sizeof(R) == 8 && (wave_fft_used(F, T, true) || UNI_EXTRA);
   using SL = Slots<F, T, NSLOT, ALIGNED>;
   using C = cx<R>;
   using Params = TrialParams<R>;
@@ -743,7 +744,16 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
       std::conditional_t<SPLITFFT, SplitFft<F, T, NBUF, R>,
                          TeamFft<F, T, NBUF, R, false, false, false, sizeof(R) == 8 && F <= 4096>>>;
   using SL = Slots<F, T, NSLOT, ALIGNED>;
-  using CHN = Channel<R, F, T, NSLOT, ALIGNED, CH>;
+  // F 4096: the SALU Philox rounds with CSI only -- CSI -2.4 %, perfect CSI +1.1 / +2.0 %
+  // (paper / paper CNC 0-8, profiles/r06/k4096/; r03 measured +1.7 % for the perfect-CSI line)
+#ifndef MIMO_UNI_4096_CSI
+#define MIMO_UNI_4096_CSI 1
+#endif
+#ifndef MIMO_UNI_8192  // A/B knob: the SALU Philox rounds at F 8192 (+1.4 % in round 3)
+#define MIMO_UNI_8192 0
+#endif
+  using CHN = Channel<R, F, T, NSLOT, ALIGNED, CH,
+                      (F == 4096 && CSI && MIMO_UNI_4096_CSI != 0) || (F == 8192 && MIMO_UNI_8192 != 0)>;
   constexpr int P = FFT::P;
   constexpr int W = T / 64;
   // Without CSI errors the channel factors as H[a,k] = f_rel[k] H'[a,k]: f_rel cancels in
@@ -757,12 +767,16 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   __shared__ R red[T / 64];  // sized by the team
   __shared__ R vk_part[2][T / 64];
   // alpha formed by one wave per antenna (array_pass): config 2 -1.0 %, CSI -1.2 %, config-5
-  // array -2.3 %; the 16-point F 4096 team +0.8 % (its register allocation again), so not
-  // there (profiles/r05/ab/ab_*_alpha1.json).  MIMO_ALPHA1=0: every wave forms it.
+  // array -2.3 % (profiles/r05/ab/ab_*_alpha1.json).  MIMO_ALPHA1=0: every wave forms it.
 #ifndef MIMO_ALPHA1
 #define MIMO_ALPHA1 1
 #endif
-  constexpr bool ALPHA1 = MIMO_ALPHA1 != 0 && F != 4096;
+  // F 4096 (fp64) since round 6, with the cold paths out of line there: -0.1 % alone, and
+  // -1.4 % / -1.0 % together with them (profiles/r06/k4096/; alone +0.8 % in round 5)
+#ifndef MIMO_ALPHA1_4096  // A/B knob
+#define MIMO_ALPHA1_4096 1
+#endif
+  constexpr bool ALPHA1 = MIMO_ALPHA1 != 0 && (F != 4096 || (MIMO_ALPHA1_4096 != 0 && sizeof(R) == 8));
   __shared__ R alpha_s[2];
   // per-antenna mean |H|^2 (CSI model): dynamic LDS of A doubles (the launch sizes it), not
   // a static kMaxCsiAnt table -- the static 4 KiB cost F 4096 its second team per CU and F
@@ -993,12 +1007,25 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // Precode with w = 1 / ||Hhat|| / sqrt(F) folded into the channel first (vk then sums
   // |Hhat w|^2 = vk / F): -1.1 % at F 2048 (wave-split instances); +5 % at F 4096, where
   // the 16-point team's register allocation suffers (profiles/r03/ab_o/ab_paper.json).
-  constexpr bool PRE_EW = SYMW_RE && WAVEFFT;
-  // General-p Rapp out of line, and the alpha fallback by the segment table (alpha_fit.h),
-  // except for the 16-point F 4096 team, where both measured slower: the outlined Rapp
-  // +1.6 % (r03 ab_s); both with the segment table +0.8 % (profiles/r04/alpha/), so it
-  // keeps the library forms inline.
-  constexpr bool COLD_OUT = sizeof(R) == 8 && F != 4096;
+  // Round 6, with the cold paths out of line: at F 4096 too (not with CSI): paper -2.8 %, paper
+  // CNC 0-8 -2.7 % on top of them; paper CSI +3.1 % (profiles/r06/k4096/)
+#ifndef MIMO_PRE_EW_4096  // A/B knob
+#define MIMO_PRE_EW_4096 1
+#endif
+#ifndef MIMO_PRE_EW_8192  // A/B knob
+#define MIMO_PRE_EW_8192 0
+#endif
+  constexpr bool PRE_EW = SYMW_RE && (WAVEFFT || (F == 4096 && !CSI && MIMO_PRE_EW_4096 != 0) ||
+                                      (F == 8192 && !CSI && MIMO_PRE_EW_8192 != 0));
+  // General-p Rapp out of line, and the alpha fallback by the segment table (alpha_fit.h).
+  // Rounds 3-5 kept the 16-point F 4096 team's library forms inline (outlined Rapp +1.6 %,
+  // r03 ab_s; with the segment table +0.8 %, profiles/r04/alpha/).  Round 6: out of line at F 4096 too -- the instance's scratch 492 -> 288 B/lane, its
+  // measured traffic 54 -> 15 KB per trial, paper -1.0 %, paper CSI -1.2 % (profiles/r06/k4096/;
+  // +1.6 % in round 3, before the later register cuts)
+#ifndef MIMO_COLD_OUT_4096  // A/B knob
+#define MIMO_COLD_OUT_4096 1
+#endif
+  constexpr bool COLD_OUT = sizeof(R) == 8 && (F != 4096 || MIMO_COLD_OUT_4096 != 0);
   // |Hhat|^2 for g recomputed after the FFT from the channel (fp64; off: +2.8 % at F 8192,
   // ab_diet_prefetch.json) -- except with CSI, where that would keep the 16-VGPR estimate
   // live across both FFTs next to the true channel: 8 VGPRs of |Hhat|^2 instead.

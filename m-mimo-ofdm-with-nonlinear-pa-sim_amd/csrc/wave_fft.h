@@ -76,7 +76,16 @@ struct WaveFft {
   static_assert(!Sub::CT || Sub::CT_N == wave_fft_ct_n(F, T), "cot-tan table layout");
   static_assert(Sub::P == P, "sub-transform keeps the points per thread");
   static constexpr int ROW = Sub::LDS_ELEMS;
+#ifdef MIMO_DIAG_ROWS2
+  // Diagnostic builds only (wrong results): the waves share two exchange rows (row w & 1), so
+  // the team's exchange LDS halves -- the occupancy A/B of 4 waves / SIMD at F 2048
+  // (profiles/r06/w4/), every access in bounds
+  static constexpr int LDS_TOTAL = 2 * ROW;
+  static __device__ __forceinline__ int row_of(int w) { return (w & 1) * ROW; }
+#else
   static constexpr int LDS_TOTAL = WV * ROW;
+  static __device__ __forceinline__ int row_of(int w) { return w * ROW; }
+#endif
   static constexpr int XCHG = 1 + Sub::XCHG;  // exchange windows per transform (fill calls)
   static constexpr int TW_INTER = wave_fft_tw_inter(F, T);
 
@@ -121,7 +130,7 @@ struct WaveFft {
       for (int k1 = 0; k1 < WV; ++k1) d[I + NB * k1] = v[k1];
     } else {
 #pragma unroll
-      for (int k1 = 0; k1 < WV; ++k1) lds[k1 * ROW + n2] = v[k1];
+      for (int k1 = 0; k1 < WV; ++k1) lds[row_of(k1) + n2] = v[k1];
     }
   }
   template <int DIR, uint32_t ZM, int I = 0>
@@ -147,13 +156,13 @@ struct WaveFft {
     const int w = tl >> 6, l = tl & 63;
     if (!no_xchg) {
       __syncthreads();
-      const C* rb = lds + w * ROW + l;
+      const C* rb = lds + row_of(w) + l;
 #pragma unroll
       for (int m = 0; m < P; ++m) d[m] = rb[64 * m];
     }
     fill(0);
     auto sub_fill = [&](int s) __attribute__((always_inline)) { fill(s + 1); };
-    Sub::template run<DIR, 0, 0u>(d, lds + w * ROW, twl, l, no_xchg, sub_fill, tw1);
+    Sub::template run<DIR, 0, 0u>(d, lds + row_of(w), twl, l, no_xchg, sub_fill, tw1);
   }
 
   // Time (as run() leaves it) -> frequency (cyclic).
@@ -167,12 +176,12 @@ struct WaveFft {
     asm volatile("" : "+s"(twl));
     asm volatile("" : "+v"(tl));
     const int w = tl >> 6, l = tl & 63;
-    Sub::template run<DIR, 0, 0u>(d, lds + w * ROW, twl, l, no_xchg, fill, tw1);
+    Sub::template run<DIR, 0, 0u>(d, lds + row_of(w), twl, l, no_xchg, fill, tw1);
     // B'[w, q] = B[w, q] e^{-j 2pi w q / F}, q = l + 64 m (wave-uniform branch)
     // (all P loads issued before the first multiply: one wait instead of P round trips).
     // The products go straight to the exchange row inside the branch: merged back into d
     // after it, they cost P register-pair copies per transform (v_mov_b64 at the join).
-    C* wb = lds + w * ROW + l;
+    C* wb = lds + row_of(w) + l;
     if (w > 0) {
       C tw[P];
 #pragma unroll
@@ -193,7 +202,7 @@ struct WaveFft {
     for (int i = 0; i < NB; ++i) {
       C v[WV];
 #pragma unroll
-      for (int w2 = 0; w2 < WV; ++w2) v[w2] = no_xchg ? d[i + NB * w2] : lds[w2 * ROW + tl + T * i];
+      for (int w2 = 0; w2 < WV; ++w2) v[w2] = no_xchg ? d[i + NB * w2] : lds[row_of(w2) + tl + T * i];
       Dft<WV, DIR>::run(v);
 #pragma unroll
       for (int k1 = 0; k1 < WV; ++k1) d[i + NB * k1] = v[k1];
