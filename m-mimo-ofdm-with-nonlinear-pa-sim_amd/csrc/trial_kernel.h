@@ -749,8 +749,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 #ifndef MIMO_UNI_4096_CSI
 #define MIMO_UNI_4096_CSI 1
 #endif
-#ifndef MIMO_UNI_8192  // A/B knob: the SALU Philox rounds at F 8192 (+1.4 % in round 3)
-#define MIMO_UNI_8192 0
+  // F 8192: on since round 6 together with the folded weight (below): config-5 array -1.6 %
+  // for both, -1.3 % for the weight alone, +0.4 % for these rounds alone (profiles/r06/k8192/;
+  // +1.4 % alone in round 3)
+#ifndef MIMO_UNI_8192  // A/B knob
+#define MIMO_UNI_8192 1
 #endif
   using CHN = Channel<R, F, T, NSLOT, ALIGNED, CH,
                       (F == 4096 && CSI && MIMO_UNI_4096_CSI != 0) || (F == 8192 && MIMO_UNI_8192 != 0)>;
@@ -1012,8 +1015,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 #ifndef MIMO_PRE_EW_4096  // A/B knob
 #define MIMO_PRE_EW_4096 1
 #endif
+  // ... and at F 8192 (not with CSI): config-5 array -1.3 %, -1.6 % with the SALU Philox rounds
+  // (profiles/r06/k8192/ab_5su.json)
 #ifndef MIMO_PRE_EW_8192  // A/B knob
-#define MIMO_PRE_EW_8192 0
+#define MIMO_PRE_EW_8192 1
 #endif
   constexpr bool PRE_EW = SYMW_RE && (WAVEFFT || (F == 4096 && !CSI && MIMO_PRE_EW_4096 != 0) ||
                                       (F == 8192 && !CSI && MIMO_PRE_EW_8192 != 0));
