@@ -1020,7 +1020,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
 #ifndef MIMO_PRE_EW_8192  // A/B knob
 #define MIMO_PRE_EW_8192 1
 #endif
-  constexpr bool PRE_EW = SYMW_RE && (WAVEFFT || (F == 4096 && !CSI && MIMO_PRE_EW_4096 != 0) ||
+  // Not with CSI since round 6: the F 2048 CSI line -1.3 % without it (profiles/r06/k2048/),
+  // as at F 4096 (+3.1 % with it)
+#ifndef MIMO_PRE_EW_CSI  // A/B knob: the folded weight in the wave-split CSI instances
+#define MIMO_PRE_EW_CSI 0
+#endif
+  constexpr bool PRE_EW = SYMW_RE && ((WAVEFFT && (!CSI || MIMO_PRE_EW_CSI != 0)) ||
+                                      (F == 4096 && !CSI && MIMO_PRE_EW_4096 != 0) ||
                                       (F == 8192 && !CSI && MIMO_PRE_EW_8192 != 0));
   // General-p Rapp out of line, and the alpha fallback by the segment table (alpha_fit.h).
   // Rounds 3-5 kept the 16-point F 4096 team's library forms inline (outlined Rapp +1.6 %,
