@@ -1040,7 +1040,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // |Hhat|^2 for g recomputed after the FFT from the channel (fp64; off: +2.8 % at F 8192,
   // ab_diet_prefetch.json) -- except with CSI, where that would keep the 16-VGPR estimate
   // live across both FFTs next to the true channel: 8 VGPRs of |Hhat|^2 instead.
-  constexpr bool E2_RE = sizeof(R) == 8 && !SYMW_LDS && !CSI;
+#ifndef MIMO_E2_RE_CSI  // A/B knob: |Hhat|^2 recomputed after the FFT with CSI too
+#define MIMO_E2_RE_CSI 0
+#endif
+  constexpr bool E2_RE = sizeof(R) == 8 && !SYMW_LDS && (!CSI || MIMO_E2_RE_CSI != 0);
   C symw_r[SYMW_LDS || SYMW_RE ? 1 : NSLOT];
   // F 8192 (one team per CU, 256 VGPRs): the lattice levels live in LDS ([slot][thread],
   // thread-private: no barrier), not in 8 VGPRs that the allocator reloaded from scratch
@@ -1049,7 +1052,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // In registers at F 4096 (256 VGPRs, 12 scratch reloads per antenna): two slots per word
   // (qam_levels8), -2.2 % on the paper config; at F 2048 (168 VGPRs, no reloads in the loop)
   // one word per slot, the packed form measured neutral to +0.3 % (profiles/r04/levels8/).
-  constexpr bool SLAB8 = SYMW_RE && !SLAB_LDS && F == 4096;
+#ifndef MIMO_SLAB8_4096  // A/B knob
+#define MIMO_SLAB8_4096 1
+#endif
+  constexpr bool SLAB8 = SYMW_RE && !SLAB_LDS && F == 4096 && MIMO_SLAB8_4096 != 0;
   uint32_t slab_r[SYMW_RE && !SLAB_LDS ? (SLAB8 ? NSLOT / 2 : NSLOT) : 1];
   __shared__ uint32_t slab_s[SLAB_LDS ? NSLOT * T : 1];
   // the lattice point of slot s (the word laundered: rebuilt per antenna, not hoisted)
