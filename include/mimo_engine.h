@@ -97,7 +97,10 @@ typedef struct mimo_point {
   double cnc_sat_pow;       /* CNC PA saturation power                                */
   double cnc_toi_coeff;     /* CNC PA cubic coefficient                               */
   double cnc_alpha;         /* CNC alpha (corrector.py:106-110)                      */
-  double csi_eps;           /* CSI error epsilon; < 0 = perfect CSI                   */
+  double csi_eps;           /* CSI error epsilon; < 0 = perfect CSI.  With CSI error: n_ant <= 512,
+                               and the run fails with MIMO_EINVAL (before any launch) if the
+                               instance's static LDS plus the n_ant-real power table exceed the
+                               CU's LDS (round 6)                                    */
   double array_alpha;       /* 0: each antenna's Bussgang gain from its precoding power
                                (Link, mp_model.py:315-317).  > 0: that gain for every antenna --
                                the TOI drivers' measured alpha_estimate
