@@ -542,8 +542,11 @@ class Link:
             if isinstance(self.my_cnc_rx, corrector.CncReceiver):
                 self.my_cnc_rx.update_distortion(ibo_db=self.ibo_val_db)
         ibo_vec = 10 * np.log10(10 ** (self.ibo_val_db / 10) * self.my_mod.n_sub_carr / (self.vk_pow_vec * self.n_ant_val))
-        ak = np.expand_dims(self.my_mod.calc_alpha(ibo_db=ibo_vec), axis=1)
-        g = np.sum(ak * self.hk_vk_agc, axis=0)
+        # sum_a ak[a] hk_vk[a, k] by einsum's own loops (no [A, S] temporary; not a BLAS
+        # matrix-vector product, whose thread pool costs ~30 ms a call on a loaded many-core
+        # host; equal to 1e-16)
+        ak = self.my_mod.calc_alpha(ibo_db=ibo_vec)
+        g = np.einsum("a,ak->k", ak, np.ascontiguousarray(self.hk_vk_agc).view(np.float64)).view(np.complex128)
         self.ak_hk_vk_noise_scaler = np.mean(np.abs(g) ** 2)
         self.ak_hk_vk_agc_nfft = np.ones(self.my_mod.n_fft, dtype=np.complex128)
         self.ak_hk_vk_agc_nfft[-(n_sc // 2):] = g[:n_sc // 2]
