@@ -297,3 +297,35 @@ def test_sixteen_antenna_cnc_and_mcnc_runs_disagree_on_the_standard_rx():
         e = np.arange(9.0, 16.0)
         a, b = (_at(np.loadtxt(os.path.join(GOLDEN, f[0]), delimiter=","), e, 2) for f in (fc, fm))
         assert np.all(np.abs(a / b - 1) <= 0.02), na
+
+
+def _ber_qam64_mrt_rayleigh(snr_mean, n_ant):
+    """The clean run's BER under MRT over n_ant i.i.d. Rayleigh antennas: the per-sub-carrier
+    SNR is snr_mean ||h_k||^2 / E||h||^2 ~ snr_mean Gamma(n_ant, 1 / n_ant) (the noise is set
+    from the mean received power, mp_model.py:159-175)."""
+    from scipy.integrate import quad
+    from scipy.stats import gamma
+    return quad(lambda x: _ber_qam64(max(snr_mean * x, 1e-300)) * gamma.pdf(x, n_ant, scale=1.0 / n_ant), 0, np.inf,
+                limit=400, epsabs=1e-14)[0]
+
+
+@pytest.mark.parametrize("n_ant", [4, 64])
+def test_rayleigh_clean_rows_match_mrt_over_independent_channels(n_ant):
+    """Parity unresolved: the 4-antenna Rayleigh curves.  What the data do show: their
+    clean rows are the stated configuration -- within 1.2 % of the closed form for MRT over 4
+    i.i.d. Rayleigh antennas, deviations of both signs (the 64-antenna files: within 0.6 %) --
+    so the mismatch sits in their distorted rows, as in the 4-antenna LoS / two-path files of
+    the same run (the same unusual Eb/N0 axis, 5-25 dB), which the band test above shows to be
+    another PA configuration."""
+    files = [f for f in sorted(os.listdir(GOLDEN))
+             if f.startswith("published_ber_vs_ebn0_") and "_rayleigh_nant%d_ibo0_" % n_ant in f]
+    assert len(files) == 2
+    for f in files:
+        a = np.loadtxt(os.path.join(GOLDEN, f), delimiter=",")
+        sel = a[1] >= 1e-3
+        th = np.array([_ber_qam64_mrt_rayleigh(6 * 10 ** (e / 10), n_ant) for e in a[0][sel]])
+        rel = a[1][sel] / th - 1
+        assert np.all(np.abs(rel) <= (0.012 if n_ant == 4 else 0.006)), f
+        assert rel.min() < 0 < rel.max(), f
+        if n_ant == 4:
+            assert a[0][-1] == 25.0  # the 4-antenna run's axis (5..25 dB), shared with its LoS / two-path files
