@@ -34,6 +34,7 @@ CASES = [
     (8192, 4, 2, 16, "softlim", 0.0, 1.0, None),
     (256, 252, 4, 16, "softlim", 0.0, 2.0, None),    # widest band allowed (S = F - 4)
     (256, 128, 2048, 64, "softlim", 0.0, 0.0, None),  # many antennas
+    (128, 64, 4096, 16, "softlim", 0.0, 1.0, None),   # the most antennas the engine takes (validate_config)
     (1024, 512, 1, 1024, "softlim", 0.0, 100.0, None),  # SISO, ideal PA, 1024-QAM
 ]
 EBN0 = {(128, 4): 6.0, (256, 128): 8.0, (1024, 512): 30.0, (2048, 8): 8.0, (4096, 8): 8.0, (8192, 4): 8.0}
