@@ -460,6 +460,24 @@ struct TeamFft {
   // (Team FFT variants measured and not taken, profiles/r05/ab/ab_*_r05e.json: the radix-16
   // stages only, stage 1's constants from an LDS copy.)
   static constexpr bool ct_stage(int s) { return CT && s >= 1; }
+  // CT_PF (A/B knob MIMO_CT_PF): the global-memory cot-tan constants of stage s + 1 loaded
+  // before stage s's exchange (their L2 latency under the barrier and the LDS round trip)
+  // instead of at the top of stage s + 1.  Off: paper +1.6 %, paper CNC 0-8 +1.7 %, config-5
+  // array +5.3 % with it (the constants held across the exchange; profiles/r06/k4096/,
+  // k8192/ab_5su_ctpf.json).
+#ifndef MIMO_CT_PF
+#define MIMO_CT_PF 0
+#endif
+  static constexpr bool CT_PF = MIMO_CT_PF != 0 && CT && !WAVE;
+  template <int S>
+  static __device__ __forceinline__ void load_ct(C (&w)[8], const C* __restrict__ tw, int t) {
+    constexpr int NS = 1 << bits_before(S);
+    constexpr int Q = ct_rows(1 << bits(S));
+    const C* cts = tw + fft_tw_total(F, P) + ct_off(S);
+    const int jm0 = t & (NS - 1);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) w[q] = gload(cts + q * NS, jm0);
+  }
   static constexpr int TWL_N = CT && WAVE ? CT_N : TW1_N + (LTW2 ? 3 * NS2 : 0);  // LDS copy
   // source index in the twiddle table of LDS-copy entry i < TWL_N (CT: relative to the
   // cot-tan region, which the caller's table places)
@@ -611,7 +629,7 @@ struct TeamFft {
   template <int S, int DIR, int PAR, uint32_t ZM, typename Fill>
   static __device__ __forceinline__ void stage(C (&d)[P], C* lds, const C* __restrict__ tw, int t,
                                                bool no_xchg, const Base& base, const Fill& fill,
-                                               const C* tw1) {
+                                               const C* tw1, C (&wct)[8]) {
     constexpr int R = 1 << bits(S);
     constexpr int NS = 1 << bits_before(S);
     constexpr int B = P / R;
@@ -623,7 +641,10 @@ struct TeamFft {
       // cot-tan constants in w0[0 .. ct_rows) (butterfly() runs dft8_ct / dft16_ct)
       static_assert(((T * (B - 1)) & (NS - 1)) == 0, "cot-tan stages: one twiddle set per thread");
       constexpr int Q = ct_rows(R);
-      if constexpr (WAVE) {
+      if constexpr (CT_PF) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) w0[q] = wct[q];  // loaded before the previous exchange
+      } else if constexpr (WAVE) {
         const C* cts = tw1 + ct_off(S) + (t & (NS - 1));
 #pragma unroll
         for (int q = 0; q < Q; ++q) w0[q] = cts[q * NS];
@@ -667,6 +688,7 @@ struct TeamFft {
     }
     butterflies<S, DIR, ZM>(d, buf, w0, t, no_xchg);
     if constexpr (!LAST) {
+      if constexpr (CT_PF && ct_stage(S + 1)) load_ct<S + 1>(wct, tw, t);
       if (!no_xchg) {
         xchg_sync<WAVE>();
         if constexpr (S == 0 && XP0) {
@@ -688,10 +710,11 @@ struct TeamFft {
 
   template <int S, int DIR, int PAR, uint32_t ZM, typename Fill>
   static __device__ __forceinline__ void stages(C (&d)[P], C* lds, const C* __restrict__ tw, int t,
-                                                bool no_xchg, const Base& base, const Fill& fill, const C* tw1) {
+                                                bool no_xchg, const Base& base, const Fill& fill, const C* tw1,
+                                                C (&wct)[8]) {
     if constexpr (S < NST) {
-      stage<S, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base, fill, tw1);
-      stages<S + 1, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base, fill, tw1);
+      stage<S, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base, fill, tw1, wct);
+      stages<S + 1, DIR, PAR, ZM>(d, lds, tw, t, no_xchg, base, fill, tw1, wct);
     }
   }
 
@@ -724,7 +747,8 @@ struct TeamFft {
     asm volatile("" : "+v"(tl));
     Base base;
     if constexpr (PREFETCH) load_base<1>(base, twl, tl);
-    stages<0, DIR, PAR, ZM>(d, lds, twl, tl, no_xchg, base, fill, tw1);
+    C wct[8];
+    stages<0, DIR, PAR, ZM>(d, lds, twl, tl, no_xchg, base, fill, tw1, wct);
   }
   // IFFT then FFT of one antenna / CNC iteration: an even number of exchanges in total.
   template <int DIR, typename Fill = NoFill>
