@@ -182,3 +182,26 @@ def test_table_channel_ignores_rx_offset_and_empty_points_launch_nothing():
     pt = dict(eng.point_kw)
     e, b, per0 = eng.run_points([pt, pt], [1, 2], [0, 5], [0, 0], [0, 1], False, per_trial=True)
     assert e.sum() == 0 and b.sum() == 0 and per0.shape == (0, 2)
+
+
+@pytest.mark.parametrize("prec", PRECISIONS)
+@pytest.mark.parametrize("F,S,receiver,csi", [(4096, 2048, "cnc", None), (4096, 2048, "mcnc", None),
+                                              (4096, 2048, "cnc", 0.2), (8192, 4096, "cnc", None),
+                                              (8192, 4096, "mcnc", None), (8192, 4096, "cnc", 0.2)])
+def test_table_channel_large_fft_vs_oracle(F, S, receiver, csi, prec):
+    """The fixed channel (MIMO_CH_TABLE) on the F 4096 / F 8192 instances, whose antenna loops
+    fold the precoding weight into the channel since round 6 (trial_kernel.h PRE_EW / WSC, the
+    non-Rayleigh form; not with CSI): exact per-trial counts vs the oracle's fixed-matrix path."""
+    rng = np.random.default_rng(78)
+    A = 8
+    h = (rng.standard_normal((A, F)) + 1j * rng.standard_normal((A, F))) * np.sqrt(0.5) * 3e-7
+    cfg = sim.SimConfig(A, S, F, 16, ibo_db=1.0, snr_db=14.0, channel="table", receiver=receiver, csi_eps=csi,
+                        table_h=h)
+    iters = [0, 1, 2]
+    n = 6
+    ref = sim.run_trials(cfg, 21, np.arange(n), iters=iters, incl_clean=True, chunk=2)
+    eng = engine_for(cfg, precision=prec)
+    _, _, per = eng.run(21, 0, n, iters, True, per_trial=True)
+    print("table large", F, receiver, csi, eng.describe(), per.sum(0), ref.sum(0))
+    assert "ch=4" in eng.describe()
+    assert_counts_equal(per, ref, f"table F={F} {receiver} {csi} {prec}")

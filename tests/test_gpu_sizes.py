@@ -70,6 +70,7 @@ CONFIG5 = [
     (8, 16, "softlim", 0.0, 1.0, "rayleigh", "mcnc", 8, None),  # MCNC array passes through the F 8192 path
     (16, 16, "softlim", 0.0, 2.0, "los", "cnc", 8, None),       # closed-form LoS on the F 8192 path
     (8, 16, "softlim", 0.0, 2.0, "rayleigh", "cnc", 8, 0.2),    # CSI (polar pass 1) on the F 8192 path
+    (16, 64, "rapp", 3.0, 3.0, "rayleigh", "mcnc", 4, None),    # config 5's PA under MCNC (the array pass per iteration)
 ]
 
 
