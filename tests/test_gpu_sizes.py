@@ -71,6 +71,8 @@ CONFIG5 = [
     (16, 16, "softlim", 0.0, 2.0, "los", "cnc", 8, None),       # closed-form LoS on the F 8192 path
     (8, 16, "softlim", 0.0, 2.0, "rayleigh", "cnc", 8, 0.2),    # CSI (polar pass 1) on the F 8192 path
     (16, 64, "rapp", 3.0, 3.0, "rayleigh", "mcnc", 4, None),    # config 5's PA under MCNC (the array pass per iteration)
+    (8, 16, "softlim", 0.0, 2.0, "two_path", "cnc", 6, None),   # two-path on the F 8192 path (folded weight, round 6)
+    (8, 16, "softlim", 0.0, 2.0, "los", "mcnc", 4, None),       # LoS MCNC on the F 8192 path
 ]
 
 
@@ -138,7 +140,7 @@ PA_PATHS = [
     (2048, 1024, "rapp", 2.5),   # general p: out of line at F 2048 (pa_rapp_general)
     (2048, 1024, "toi", 0.0),
     (4096, 2048, "rapp", 3.0),
-    (4096, 2048, "rapp", 2.5),   # general p: inline at F 4096 (COLD_OUT off)
+    (4096, 2048, "rapp", 2.5),   # general p: out of line at F 4096 too since round 6 (COLD_OUT)
     (4096, 2048, "toi", 0.0),
 ]
 
@@ -147,8 +149,8 @@ PA_PATHS = [
 @pytest.mark.parametrize("F,S,pa,p", PA_PATHS)
 def test_pa_paths_per_instance_vs_oracle(F, S, pa, p, prec):
     """Every PA branch of pa_block() in the F 2048 and F 4096 instances (the PA kind is a
-    run-time switch inside one instance, and the general-p Rapp is out of line at F 2048 but
-    inline at F 4096): per-trial counts EXACTLY equal to the oracle's."""
+    run-time switch inside one instance; the general-p Rapp is out of line in both since round
+    6): per-trial counts EXACTLY equal to the oracle's."""
     A, M = 8, 64
     snr = float(sim.rm.ebn0_to_snr(12.0, S, S, M))
     cfg = sim.SimConfig(A, S, F, M, pa=pa, p_hardness=p, ibo_db=1.5, snr_db=snr)
