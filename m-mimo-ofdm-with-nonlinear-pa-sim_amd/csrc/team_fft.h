@@ -22,6 +22,7 @@
 
 #include <type_traits>
 
+#include "tuning.h"
 #include "real.h"
 
 
@@ -465,9 +466,6 @@ struct TeamFft {
   // instead of at the top of stage s + 1.  Off: paper +1.6 %, paper CNC 0-8 +1.7 %, config-5
   // array +5.3 % with it (the constants held across the exchange; profiles/r06/k4096/,
   // k8192/ab_5su_ctpf.json).
-#ifndef MIMO_CT_PF
-#define MIMO_CT_PF 0
-#endif
   static constexpr bool CT_PF = MIMO_CT_PF != 0 && CT && !WAVE;
   template <int S>
   static __device__ __forceinline__ void load_ct(C (&w)[8], const C* __restrict__ tw, int t) {

@@ -41,9 +41,6 @@ constexpr Profile profile_for(int T, bool aligned, int ch) {
   // fp64 up to F 2048: 3 waves/SIMD (168 VGPRs; the symbols rebuilt from the labels and
   // |Hhat|^2 after the FFT, so 49.5 KiB of LDS per 256-thread team and 3 teams per CU):
   // -8.5 % at config 2 (profiles/r03/ab_w3/).
-#ifndef MIMO_W64_2048  // A/B knob (make variant VFLAGS=-DMIMO_W64_2048=4)
-#define MIMO_W64_2048 3
-#endif
   if (kF64 && kF <= 2048) return Profile{MIMO_W64_2048, 1, false};
   if (kF64 && kF == 4096) return Profile{2, 1, false};  // 16-point team, symbols from levels: 2 teams/CU
   if (kF64) return Profile{2, 1, true};

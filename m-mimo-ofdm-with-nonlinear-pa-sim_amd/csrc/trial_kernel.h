@@ -30,6 +30,7 @@
 
 #include <type_traits>
 
+#include "tuning.h"
 #include "alpha_fit.h"
 #include "philox.h"
 #include "team_fft.h"
@@ -746,15 +747,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   using SL = Slots<F, T, NSLOT, ALIGNED>;
   // F 4096: the SALU Philox rounds with CSI only -- CSI -2.4 %, perfect CSI +1.1 / +2.0 %
   // (paper / paper CNC 0-8, profiles/r06/k4096/; r03 measured +1.7 % for the perfect-CSI line)
-#ifndef MIMO_UNI_4096_CSI
-#define MIMO_UNI_4096_CSI 1
-#endif
   // F 8192: on since round 6 together with the folded weight (below): config-5 array -1.6 %
   // for both, -1.3 % for the weight alone, +0.4 % for these rounds alone (profiles/r06/k8192/;
   // +1.4 % alone in round 3)
-#ifndef MIMO_UNI_8192  // A/B knob
-#define MIMO_UNI_8192 1
-#endif
   using CHN = Channel<R, F, T, NSLOT, ALIGNED, CH,
                       (F == 4096 && CSI && MIMO_UNI_4096_CSI != 0) || (F == 8192 && MIMO_UNI_8192 != 0)>;
   constexpr int P = FFT::P;
@@ -771,14 +766,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   __shared__ R vk_part[2][T / 64];
   // alpha formed by one wave per antenna (array_pass): config 2 -1.0 %, CSI -1.2 %, config-5
   // array -2.3 % (profiles/r05/ab/ab_*_alpha1.json).  MIMO_ALPHA1=0: every wave forms it.
-#ifndef MIMO_ALPHA1
-#define MIMO_ALPHA1 1
-#endif
   // F 4096 (fp64) since round 6, with the cold paths out of line there: -0.1 % alone, and
   // -1.4 % / -1.0 % together with them (profiles/r06/k4096/; alone +0.8 % in round 5)
-#ifndef MIMO_ALPHA1_4096  // A/B knob
-#define MIMO_ALPHA1_4096 1
-#endif
   constexpr bool ALPHA1 = MIMO_ALPHA1 != 0 && (F != 4096 || (MIMO_ALPHA1_4096 != 0 && sizeof(R) == 8));
   __shared__ R alpha_s[2];
   // per-antenna mean |H|^2 (CSI model): dynamic LDS of A doubles (the launch sizes it), not
@@ -883,9 +872,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   }
   const bool clean_cc = CSI && p.incl_clean;
   // pass 1 of the Rayleigh CSI instances in polar form (below; MIMO_CSI_POLAR=0: Cartesian)
-#ifndef MIMO_CSI_POLAR
-#define MIMO_CSI_POLAR 1
-#endif
   constexpr bool CSI_POLAR = MIMO_CSI_POLAR != 0 && CSI && CH == CH_RAYLEIGH && ALIGNED && sizeof(R) == 8;
   for (int a = 0; a < (MIMO_ABL(p, ABL_PASS1) ? 1 : A); ++a) {
     MIMO_ISA_MARK("pass1");
@@ -1012,19 +998,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // the 16-point team's register allocation suffers (profiles/r03/ab_o/ab_paper.json).
   // Round 6, with the cold paths out of line: at F 4096 too (not with CSI): paper -2.8 %, paper
   // CNC 0-8 -2.7 % on top of them; paper CSI +3.1 % (profiles/r06/k4096/)
-#ifndef MIMO_PRE_EW_4096  // A/B knob
-#define MIMO_PRE_EW_4096 1
-#endif
   // ... and at F 8192 (not with CSI): config-5 array -1.3 %, -1.6 % with the SALU Philox rounds
   // (profiles/r06/k8192/ab_5su.json)
-#ifndef MIMO_PRE_EW_8192  // A/B knob
-#define MIMO_PRE_EW_8192 1
-#endif
   // Not with CSI since round 6: the F 2048 CSI line -1.3 % without it (profiles/r06/k2048/),
   // as at F 4096 (+3.1 % with it)
-#ifndef MIMO_PRE_EW_CSI  // A/B knob: the folded weight in the wave-split CSI instances
-#define MIMO_PRE_EW_CSI 0
-#endif
   constexpr bool PRE_EW = SYMW_RE && ((WAVEFFT && (!CSI || MIMO_PRE_EW_CSI != 0)) ||
                                       (F == 4096 && !CSI && MIMO_PRE_EW_4096 != 0) ||
                                       (F == 8192 && !CSI && MIMO_PRE_EW_8192 != 0));
@@ -1033,16 +1010,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // r03 ab_s; with the segment table +0.8 %, profiles/r04/alpha/).  Round 6: out of line at F 4096 too -- the instance's scratch 492 -> 288 B/lane, its
   // measured traffic 54 -> 15 KB per trial, paper -1.0 %, paper CSI -1.2 % (profiles/r06/k4096/;
   // +1.6 % in round 3, before the later register cuts)
-#ifndef MIMO_COLD_OUT_4096  // A/B knob
-#define MIMO_COLD_OUT_4096 1
-#endif
   constexpr bool COLD_OUT = sizeof(R) == 8 && (F != 4096 || MIMO_COLD_OUT_4096 != 0);
   // |Hhat|^2 for g recomputed after the FFT from the channel (fp64; off: +2.8 % at F 8192,
   // ab_diet_prefetch.json) -- except with CSI, where that would keep the 16-VGPR estimate
   // live across both FFTs next to the true channel: 8 VGPRs of |Hhat|^2 instead.
-#ifndef MIMO_E2_RE_CSI  // A/B knob: |Hhat|^2 recomputed after the FFT with CSI too
-#define MIMO_E2_RE_CSI 0
-#endif
   constexpr bool E2_RE = sizeof(R) == 8 && !SYMW_LDS && (!CSI || MIMO_E2_RE_CSI != 0);
   C symw_r[SYMW_LDS || SYMW_RE ? 1 : NSLOT];
   // F 8192 (one team per CU, 256 VGPRs): the lattice levels live in LDS ([slot][thread],
@@ -1052,9 +1023,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   // In registers at F 4096 (256 VGPRs, 12 scratch reloads per antenna): two slots per word
   // (qam_levels8), -2.2 % on the paper config; at F 2048 (168 VGPRs, no reloads in the loop)
   // one word per slot, the packed form measured neutral to +0.3 % (profiles/r04/levels8/).
-#ifndef MIMO_SLAB8_4096  // A/B knob
-#define MIMO_SLAB8_4096 1
-#endif
   constexpr bool SLAB8 = SYMW_RE && !SLAB_LDS && F == 4096 && MIMO_SLAB8_4096 != 0;
   uint32_t slab_r[SYMW_RE && !SLAB_LDS ? (SLAB8 ? NSLOT / 2 : NSLOT) : 1];
   __shared__ uint32_t slab_s[SLAB_LDS ? NSLOT * T : 1];
@@ -1110,9 +1078,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(MINW))) void 
   constexpr bool WSC = PRE_EW && !CSI;
   // ... and for the Rayleigh channel the weight is folded into the Box-Muller radius
   // (CHN::normals_w): one multiply per draw instead of three, |h w|^2 from the radius
-#ifndef MIMO_WSC_RAY
-#define MIMO_WSC_RAY 1
-#endif
   constexpr bool WSC_RAY = MIMO_WSC_RAY != 0 && WSC && CH == CH_RAYLEIGH && ALIGNED;  // (fp64: no pipelined draws)
   R wsc[WSC ? NSLOT : 1];
   auto array_pass = [&](bool main_pass, C (&acc)[NSLOT]) __attribute__((always_inline)) {
