@@ -142,6 +142,8 @@ PA_PATHS = [
     (4096, 2048, "rapp", 3.0),
     (4096, 2048, "rapp", 2.5),   # general p: out of line at F 4096 too since round 6 (COLD_OUT)
     (4096, 2048, "toi", 0.0),
+    (2048, 1024, "rapp", 5.0),   # the hardness the reference's plots use
+    (8192, 4096, "rapp", 4.0),   # the hardness of its commented-out driver line, on the F 8192 instance
 ]
 
 
