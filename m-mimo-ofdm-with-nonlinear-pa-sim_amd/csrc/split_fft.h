@@ -28,12 +28,7 @@
 
 namespace mimo {
 
-#ifndef MIMO_SPLIT_FFT
-#define MIMO_SPLIT_FFT 1
-#endif
-#ifndef MIMO_SPLIT_CT
-#define MIMO_SPLIT_CT 1
-#endif
+// (MIMO_SPLIT_FFT / MIMO_SPLIT_CT: tuning.h)
 constexpr bool kSplitCt = MIMO_SPLIT_CT != 0;  // the sub-transforms' stages in cot-tan form
 constexpr bool split_fft_used(int F, int T, bool f64) { return MIMO_SPLIT_FFT != 0 && f64 && F == 8192 && T == 512; }
 // table layout (engine.hip split_twiddles)

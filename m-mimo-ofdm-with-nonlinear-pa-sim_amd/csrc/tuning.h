@@ -82,6 +82,16 @@
 #define MIMO_SLAB8_4096 1
 #endif
 
+// ---- fp64 F 8192 (split_fft.h): two 4096-point sub-transforms on the lane halves and a
+// radix-2 stage through v_permlane32_swap: -6.2 % against the 8192-point team (0: the team);
+// their stages in cot-tan form: -2.4 % (profiles/r05/split/ab_5su_split.json).
+#ifndef MIMO_SPLIT_FFT
+#define MIMO_SPLIT_FFT 1
+#endif
+#ifndef MIMO_SPLIT_CT
+#define MIMO_SPLIT_CT 1
+#endif
+
 // ---- team FFT (team_fft.h): the cot-tan constants of stage s + 1 loaded before stage s's
 // exchange: paper +1.6 %, config-5 array +5.3 % (profiles/r06/k4096/, k8192/ab_5su_ctpf.json).
 #ifndef MIMO_CT_PF
