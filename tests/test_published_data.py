@@ -329,3 +329,55 @@ def test_rayleigh_clean_rows_match_mrt_over_independent_channels(n_ant):
         assert rel.min() < 0 < rel.max(), f
         if n_ant == 4:
             assert a[0][-1] == 25.0  # the 4-antenna run's axis (5..25 dB), shared with its LoS / two-path files
+
+
+# ---------------------------------------------------------------------------------------
+# The three-cornered hat (tools/published_families.py tch_solve) on synthetic data of known
+# scatter factors and bias: the published-pair GPU test (test_gpu_published_pairs.py) rests on
+# it recovering them.
+
+def _tch_synthetic(k_a, k_b, bias_in_sig_a, seed, n_pts=16, n_rows=10, n_tr=8192):
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import published_families as pf
+    rng = np.random.default_rng(seed)
+    p = 10 ** rng.uniform(-4, -1.5, (n_rows, n_pts))
+    sd = 1.5 * np.sqrt(p / BPS)                      # per-trial spread, a little above binomial
+    n_a = np.minimum(2442.0, np.ceil(1e7 / (p * BPS)))
+    n_b = np.minimum(2442.0, np.ceil(1e6 / (p * BPS)))
+    sig_a = sd * np.sqrt(1.0 / n_a)
+    e = p + bias_in_sig_a * sig_a + rng.standard_normal(p.shape) * sd / np.sqrt(n_tr)
+    a = p + rng.standard_normal(p.shape) * sd * np.sqrt(k_a / n_a)
+    b = p + rng.standard_normal(p.shape) * sd * np.sqrt(k_b / n_b)
+    return pf.tch_solve(e, sd, a, b, n_tr, n_a, n_b, np.ones_like(p, bool), n_boot=300)
+
+
+@pytest.mark.parametrize("k_a,k_b,bias", [(1.0, 1.0, 0.0), (3.0, 1.5, 0.0), (2.0, 0.8, 1.0)])
+def test_tch_recovers_scatter_and_bias(k_a, k_b, bias):
+    hits = []
+    for seed in range(6):
+        r = _tch_synthetic(k_a, k_b, bias, seed)
+        hits.append(abs(r["k_a"] - k_a) <= 3 * r["se_k_a"] and abs(r["k_b"] - k_b) <= 3 * r["se_k_b"]
+                    and abs(r["beta"] - bias ** 2) <= 3 * r["se_beta"] + 0.05)
+    assert sum(hits) >= 5, hits
+
+
+def test_tch_detects_a_bias():
+    # an engine 0.8 published sigma off on every point is flagged at 2 standard errors (at 16
+    # points x 10 rows the standard error of beta is ~0.15: the resolution is ~0.55 sigma)
+    r = _tch_synthetic(2.0, 1.0, 0.8, seed=11, n_pts=16)
+    assert r["beta"] - 2 * r["se_beta"] > 0, r
+    r0 = _tch_synthetic(2.0, 1.0, 0.0, seed=11, n_pts=16)
+    assert r0["beta"] - 2 * r0["se_beta"] <= 0, r0
+
+
+def test_tch_pairs_are_the_same_quantity():
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import published_families as pf
+    ps = pf.pairs()
+    assert len(ps) == 16
+    for p in ps:
+        a, b = p["a"], p["b"]
+        assert (a["receiver"], a["channel"]) == (b["receiver"], b["channel"]) or p["rows"] == [0, 1]
+        assert a["channel"] == b["channel"] and a.get("eps") == b.get("eps") and a.get("ibo") == b.get("ibo")
+        axa, axb = (np.loadtxt(os.path.join(GOLDEN, "published_" + c["file"] + ".csv"), delimiter=",")[0] for c in (a, b))
+        assert sum(np.any(np.isclose(axb, x)) for x in axa) >= 16

@@ -16,6 +16,7 @@
 #   bash tools/gpu.sh c4 <out> [fixed_ber_check args]  config-4 grids (tools/fixed_ber_check.py)
 #   bash tools/gpu.sh families <out> [family]          published CSI / BER-vs-IBO / small-array curves
 #                                                      (tools/published_families.py)
+#   bash tools/gpu.sh pairs <out>                      three-cornered hat over published re-runs
 set -o pipefail
 export TMPDIR=/tmp
 MODE=$1; O=$2; shift 2
@@ -96,6 +97,8 @@ case $MODE in
     fam=${1:-all}
     timeout -k 10 900 python -u tools/published_families.py --family $fam --out "$O/families_$fam.json" > "$O/families_$fam.log" 2> "$O/families_$fam.err" || exit $?
     python -c "import json; [print(d['curve'], d['compared'], d['frac_abs_z_le1'], d['mean_z2'], d['max_abs_z'], d['median_abs_rel'], d['min_p_zero'], d['layout'], {k: v['mean_z2'] for k, v in d.items() if k.startswith('alt_')}) for d in json.load(open('$O/families_$fam.json'))]" ;;
+  pairs)  # the three-cornered hat over the published re-run pairs + the calibrated csi1 curves
+    timeout -k 10 900 python -u tools/published_families.py --pairs --out "$O/pairs.json" > "$O/pairs.log" 2> "$O/pairs.err" || exit $? ;;
   *)
     echo "unknown mode $MODE"; exit 2 ;;
 esac

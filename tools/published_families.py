@@ -286,11 +286,13 @@ def run_engine(link, pts, n_tr, seed0, precision=None):
     return err, bits, per.reshape(n_pt, n_tr, len(ITERS) + 1), dt
 
 
-def compare(ber, sd, q, pub, n_tr, bits_max, n_err_min, err):
-    """z statistics, bias and zero-region figures of one curve ([counter, point] arrays)."""
+def compare(ber, sd, q, pub, n_tr, bits_max, n_err_min, err, k_ref=1.0):
+    """z statistics, bias and zero-region figures of one curve ([counter, point] arrays).
+    ``k_ref`` scales the published value's variance (1: the stated stopping rule; a scatter
+    factor measured from the published re-runs, tch(), otherwise)."""
     n_ref = stop_trials(ber, bits_max, n_err_min)
     sig_gpu = sd / np.sqrt(n_tr)
-    sig_ref = sd / np.sqrt(n_ref)
+    sig_ref = sd * np.sqrt(k_ref / n_ref)
     ref_errs = pub * n_ref * BPS
     sel = (pub >= 1e-5) & (ref_errs >= 100) & (sd > 0)
     z = (ber - pub) / np.sqrt(sig_gpu ** 2 + sig_ref ** 2 + 1e-300)
@@ -325,7 +327,7 @@ def compare(ber, sd, q, pub, n_tr, bits_max, n_err_min, err):
     return out, z, sel
 
 
-def measure(c, n_tr=None, seed0=5150, f32_check=False):
+def measure(c, n_tr=None, seed0=5150, f32_check=False, k_ref=1.0):
     """The engine's estimate of every counter of every point of curve ``c`` against the
     published one.  Returns (summary dict, arrays)."""
     axis, pub = published(c)
@@ -346,7 +348,8 @@ def measure(c, n_tr=None, seed0=5150, f32_check=False):
     arrays = None
     for name in maps:
         cols = ROW_MAPS[name](R)
-        st, z, sel = compare(ber[cols], sd[cols], q[cols], pub, n_tr, c["bits_max"], c["n_err_min"], err.T[cols])
+        st, z, sel = compare(ber[cols], sd[cols], q[cols], pub, n_tr, c["bits_max"], c["n_err_min"], err.T[cols],
+                             k_ref)
         if name == main:
             out.update(st)
             out["z_map"] = [[round(float(v), 2) if s else None for v, s in zip(zr, sr)] for zr, sr in zip(z, sel)]
@@ -360,9 +363,99 @@ def measure(c, n_tr=None, seed0=5150, f32_check=False):
         out["f32_total_err_ratio"] = round(float(e32.sum() / max(1, err.sum())), 6)
         cols = ROW_MAPS[main](R)
         st32, _, _ = compare((e32 / b32).T[cols], sd[cols], q[cols], pub, n_tr, c["bits_max"], c["n_err_min"],
-                             e32.T[cols])
+                             e32.T[cols], k_ref)
         out["f32_mean_z2"], out["f32_compared"] = st32["mean_z2"], st32["compared"]
     return out, arrays
+
+
+# ---------------------------------------------------------------------------------------
+# Three-cornered hat over published re-runs.  Where the reference published two independent
+# runs of the same quantity -- the step-1 CSI files (csi1) re-run the 0.5-dB CSI files (csi)
+# at eps 0 .. 0.4; a CNC and an MCNC file hold the same no-distortion and standard-RX rows --
+# the engine and the two runs are three estimates of one value.  Per point, in units of the
+# engine's per-trial spread sd and of run A's stopping-rule trial count n_a (rho = n_a / n_b):
+#   U = n_a ((e - a) / sd)^2 = n_a / n_tr + k_a + beta
+#   V = n_a ((e - b) / sd)^2 = n_a / n_tr + k_b rho + beta
+#   W = n_a ((a - b) / sd)^2 =              k_a + k_b rho
+# k_a, k_b: each run's variance against its stated stopping rule's (1: the rule holds);
+# beta: the engine's squared bias in units of run A's sigma^2.  Least squares over the points,
+# standard errors by resampling whole points (the rows of a point share their trials).  No
+# stopping-rule assumption enters beta: the two runs' own disagreement calibrates it.
+
+
+def pairs():
+    """The published re-run pairs (run A, run B, rows both files hold for the same quantity)."""
+    by = {(c["family"], c["receiver"], c["channel"], c.get("eps"), c.get("ibo")): c for c in CURVES}
+    out = []
+    for rx in ("cnc", "mcnc"):
+        for eps in (0.0, 0.1, 0.2, 0.3, 0.4):
+            out.append(dict(name="csi1_vs_csi_%s_los_eps%.1f" % (rx, eps), a=by[("csi1", rx, "los", eps, 0.0)],
+                            b=by[("csi", rx, "los", eps, 0.0)], rows=list(range(len(ITERS) + 1))))
+    for ibo in (1.0, 0.0):
+        for ch in ("los", "two_path", "rayleigh"):
+            out.append(dict(name="ebn0_ibo%g_%s_cnc_vs_mcnc" % (ibo, ch), a=by[("ebn0", "cnc", ch, None, ibo)],
+                            b=by[("ebn0", "mcnc", ch, None, ibo)], rows=[0, 1]))
+    return out
+
+
+def tch_solve(ber, sd, pa, pb, n_tr, n_a, n_b, sel, n_boot=1000, seed=0):
+    """(k_a, k_b, beta) and their resampling standard errors from [row, point] arrays
+    (``sel``: the cells compared)."""
+    cols = np.flatnonzero(sel.any(axis=0))
+    if cols.size < 4:
+        return None
+
+    def fit(idx):
+        s = sel[:, idx]
+        e, d, a, b = ber[:, idx][s], sd[:, idx][s], pa[:, idx][s], pb[:, idx][s]
+        na, rho = n_a[:, idx][s], (n_a / n_b)[:, idx][s]
+        off = na / n_tr
+        U, V, W = na * ((e - a) / d) ** 2 - off, na * ((e - b) / d) ** 2 - off, na * ((a - b) / d) ** 2
+        one, zero = np.ones_like(U), np.zeros_like(U)
+        X = np.concatenate([np.stack([one, zero, one], 1), np.stack([zero, rho, one], 1), np.stack([one, rho, zero], 1)])
+        return np.linalg.lstsq(X, np.concatenate([U, V, W]), rcond=None)[0]
+
+    est = fit(cols)
+    rng = np.random.default_rng(seed)
+    boot = np.array([fit(rng.choice(cols, cols.size)) for _ in range(n_boot)])
+    se = boot.std(axis=0, ddof=1)
+    return dict(k_a=round(float(est[0]), 4), k_b=round(float(est[1]), 4), beta=round(float(est[2]), 4),
+                se_k_a=round(float(se[0]), 4), se_k_b=round(float(se[1]), 4), se_beta=round(float(se[2]), 4),
+                points=int(cols.size), cells=int(sel.sum()))
+
+
+def tch(p, n_tr=None, seed0=5150):
+    """The engine at the common points of a published pair; tch_solve's figures, plus each run's
+    effective trial count (its rule's median over k)."""
+    ca, cb = p["a"], p["b"]
+    axa, puba = published(ca)
+    axb, pubb = published(cb)
+    common = np.array([x for x in axa if np.any(np.isclose(axb, x))])
+    ia = [int(np.flatnonzero(np.isclose(axa, x))[0]) for x in common]
+    ib = [int(np.flatnonzero(np.isclose(axb, x))[0]) for x in common]
+    if n_tr is None:
+        n_tr = 4096 if ca["receiver"] == "mcnc" else 8192
+    link, pts = points(ca, common)
+    err, bits, per, dt = run_engine(link, pts, n_tr, seed0)
+    rows = p["rows"]
+    cols_a = ROW_MAPS[layout(ca, axa, puba)](puba.shape[0])
+    ber = (err / bits).T[cols_a][rows]
+    sd = (per.astype(np.float64) / BPS).std(axis=1, ddof=1).T[cols_a][rows]
+    pa, pb = puba[rows][:, ia], pubb[rows][:, ib]
+    n_a = stop_trials(ber, ca["bits_max"], ca["n_err_min"])
+    n_b = stop_trials(ber, cb["bits_max"], cb["n_err_min"])
+    sel = (pa >= 1e-5) & (pb >= 1e-5) & (pa * n_a * BPS >= 100) & (pb * n_b * BPS >= 100) & (sd > 0)
+    out = dict(pair=p["name"], a=ca["file"], b=cb["file"], n_tr=n_tr, points=len(common), rows=len(rows),
+               seconds=round(dt, 2))
+    res = tch_solve(ber, sd, pa, pb, n_tr, n_a, n_b, sel)
+    if res is not None:
+        out.update(res)
+        out["n_rule_a"], out["n_rule_b"] = float(np.median(n_a[sel])), float(np.median(n_b[sel]))
+        out["n_eff_a"] = round(out["n_rule_a"] / max(res["k_a"], 1e-9), 1)
+        out["n_eff_b"] = round(out["n_rule_b"] / max(res["k_b"], 1e-9), 1)
+        # the bias the engine may still have at 2 standard errors, in units of run A's sigma
+        out["bias_rms_2se"] = round(float(np.sqrt(max(0.0, res["beta"] + 2 * res["se_beta"]))), 4)
+    return out
 
 
 def main():
@@ -370,7 +463,30 @@ def main():
     ap.add_argument("--family", default="all")
     ap.add_argument("--out", default=None)
     ap.add_argument("--n-tr", type=int, default=None)
+    ap.add_argument("--pairs", action="store_true", help="the three-cornered hat over the published re-run pairs")
     a = ap.parse_args()
+    if a.pairs:
+        res = []
+        for p in pairs():
+            r = tch(p, a.n_tr)
+            print(json.dumps(r), flush=True)
+            res.append(r)
+        # the csi1 runs' scatter factor, pooled per receiver over the paired eps 0 .. 0.4 runs,
+        # applied to every csi1 curve (the unpaired ones are the same driver revision's runs)
+        for rx in ("cnc", "mcnc"):
+            ks = [r["k_a"] for r in res if r["pair"].startswith("csi1_vs_csi_%s_" % rx) and "k_a" in r]
+            k = float(np.median(ks))
+            for c in CURVES:
+                if c["family"] == "csi1" and c["receiver"] == rx:
+                    r, _ = measure(c, a.n_tr, k_ref=k)
+                    r = {kk: v for kk, v in r.items() if kk != "z_map"}
+                    r["k_ref"] = round(k, 4)
+                    print(json.dumps(r), flush=True)
+                    res.append(r)
+        if a.out:
+            with open(a.out, "w") as f:
+                json.dump(res, f, indent=1)
+        return
     res = []
     for c in CURVES:
         if a.family != "all" and c["family"] != a.family:
