@@ -13,10 +13,9 @@ the same on every box.  Groups:
   no counter row whose mean z leaves +-2: MCNC with CSI error (5 eps), BER vs IBO over
   LoS at Eb/N0 15 and 1000 (CNC, MCNC), over Rayleigh (CNC, MCNC) and two-path (MCNC) at
   64 antennas, and the 1-antenna LoS / two-path curves (CNC, MCNC).
-* CSI_CNC -- CNC with CSI error: no bias (every counter row within +-0.75 % and +-0.6 z),
-  but a scatter of 1.1-2.8 x the stated rule's prediction (n_eff 750-2100 trials against
-  its 2,442; the same per-point excess as the config-4 grids): mean z^2 <= 3,
-  >= 75 % within 2 sigma.
+* CNC with CSI error (0.5-dB runs) and the step-1 CNC / Rayleigh-MCNC CSI runs: their scatter
+  exceeds the stated stopping rule's, so they are compared in tests/test_gpu_published_pairs.py
+  with a published sigma calibrated by the reference's own re-runs (three-cornered hat).
 * FIT also holds the BER-vs-Eb/N0 curves at IBO 1 (the committed drivers' own setting) and
   IBO 0 (family ebn0: LoS, two-path, Rayleigh x CNC, MCNC) and 32 more BER-vs-IBO files
   (family ibo2: Eb/N0 10-20 and 1000 dB, IBO -9..9 included; row layout read from the data,
@@ -24,18 +23,11 @@ the same on every box.  Groups:
   (mean z^2 ~1) but whose few-error points put the median |rel| at 3-4 %: the FIT z bounds with
   a 5 % median.  The noiseless ibo2 files (IBO down to -9 dB) hold float32 to >= 99.7 %.
 * FIT also: the 1-antenna LoS / two-path BER-vs-Eb/N0 curves at IBO 0 (family small2, CNC);
-  FIT_OUTLIER: their MCNC files (0.5-dB steps), the FIT bounds but for max |z|: one isolated
+  FIT_OUTLIER: their MCNC files (0.5-dB steps), the FIT bounds but for max |z|: at most one isolated
   point each (z -14 at iteration 5, 18.5 dB; the no-distortion row at 8 dB, z 6.5).  Not
   compared in small2: the 1-antenna Rayleigh and 4-antenna curves (as in the IBO families),
   the 16-antenna files (5 points), LoS IBO 50 (its no-distortion row reads BER 0.79-0.83, a
   broken clean run; its distorted rows agree within 0.6 %) and two-path IBO 20 (5-18 % apart).
-* CSI1_BIAS -- the step-1 CSI runs (family csi1: other revisions of the CSI drivers) with CNC
-  over LoS (eps 0 .. 0.7) and Rayleigh (eps 0.01 .. 0.2), and MCNC over Rayleigh: no bias
-  (median |rel| <= 0.5 %, every counter row's mean relative difference within +-2 %), but
-  their scatter exceeds the assumed stopping rule's (n_eff 200-1170 trials against its
-  2,442 -- those revisions' bits_sent_max is not known), so only loose z bounds.  The MCNC
-  LoS step-1 runs scatter exactly as the rule predicts (n_eff within 0.6-1.7 x n_ref) and
-  are in FIT.
 * Not compared (the z maps in profiles/r05/families/).  Every exclusion but one
   is backed by the published files alone, in tests/test_published_data.py (CPU): the CNC LoS /
   two-path IBO 0..8 files (below every other run of the same quantities), the 4-antenna LoS /
@@ -76,9 +68,9 @@ def _group(c):
             return None
         return "fit" if c["receiver"] == "cnc" else "fit_outlier"
     if c["family"] == "csi" and c["receiver"] == "cnc":
-        return "csi_cnc"
+        return None  # calibrated by the published re-runs: tests/test_gpu_published_pairs.py
     if c["family"] == "csi1" and (c["receiver"] == "cnc" or c["channel"] == "rayleigh"):
-        return "csi1_bias"
+        return None  # likewise
     if name in FIT_LOWCOUNT:
         return "fit_lowcount"
     return "fit"
@@ -103,19 +95,6 @@ def test_published_family_curve(c):
             assert len(far) <= 1, far
         for row, mz in out["row_mean_z"].items():
             assert abs(mz) <= 2.0, (row, mz)
-    elif g == "csi1_bias":
-        assert out["median_abs_rel"] <= 0.005
-        assert out["mean_z2"] <= 12.0 and out["frac_abs_z_le2"] >= 0.5
-        for row, rel in out["row_mean_rel"].items():
-            assert abs(rel) <= 0.02, (row, rel)
-        for row, mz in out["row_mean_z"].items():
-            assert abs(mz) <= 3.0, (row, mz)
-    else:
-        assert out["mean_z2"] <= 3.0 and out["frac_abs_z_le2"] >= 0.75
-        for row, rel in out["row_mean_rel"].items():
-            assert abs(rel) <= 0.0075, (row, rel)
-        for row, mz in out["row_mean_z"].items():
-            assert abs(mz) <= 0.6, (row, mz)
     # zero region: published 0 must be likely under the engine's rate of erroneous trials
     assert out["min_p_zero"] >= 1e-3
     if noiseless and c["family"] == "ibo":
