@@ -227,14 +227,16 @@ def launch_ranks(n):
     return proc.returncode
 
 
-def time_grid(rank, world, dist, dev, precision, tdev, fake=False):
+def time_grid(rank, world, dist, dev, precision, tdev, fake=False, split="points"):
     """North_star's multi-GPU split (BASELINE config 4): ``sweep.run_grid`` over the 915-point
     SNR x IBO extent (sweep.BASELINE_C4), grid points dealt over the N ranks by estimated cost
     (LPT), one all-reduce of the counters -- exactly what the reference's fixed-BER driver runs
     point by point on one host (main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:100-215).
     Strong scaling: the grid is fixed, N ranks share it.  Timed between barriers after an
     untimed engine set-up; the wall time is the MAX over ranks.  ``fake``: the CPU rehearsal
-    (tests/fake_link.py stand-in, no GPU) of the same plumbing."""
+    (tests/fake_link.py stand-in, no GPU) of the same plumbing.  ``split="trials"``
+    (``--grid-split trials``): the ranks share every point's trials instead, one all-reduce per
+    stopping-rule round (same counts digest)."""
     import hashlib
 
     import sweep
@@ -252,7 +254,7 @@ def time_grid(rank, world, dist, dev, precision, tdev, fake=False):
     t0 = time.perf_counter()
     st = {}
     err, bits = sweep.run_grid(link, c4["ibo"], c4["ebn0"], c4["iters"], incl_clean=False, seed=2137, rank=rank,
-                               world=world, dist=dist, device=dev, stats=st)
+                               world=world, dist=dist, device=dev, stats=st, split=split)
     if not fake:
         import torch
         torch.cuda.synchronize()
@@ -288,7 +290,9 @@ def time_grid(rank, world, dist, dev, precision, tdev, fake=False):
                     "BASELINE's 'SNR 0-30 dB' read as Eb/N0: SNR = Eb/N0 + 7.8 dB at 64-QAM)",
             "points": int(len(c4["ibo"]) * len(c4["ebn0"])), "ofdm_symbols": n_sym, "wall_s": round(dt, 4),
             "symbols_per_s": round(n_sym / dt, 1), "ranks_seen": ranks, "scaling": "strong",
-            "parallelism": f"points dealt by cost (LPT) over {world} rank(s), one all-reduce of the counters",
+            "parallelism": (f"points dealt by cost (LPT) over {world} rank(s), one all-reduce of the counters"
+                            if split == "points" or not dist else
+                            f"every point's trials shared by {world} rank(s), one all-reduce per stopping-rule round"),
             "per_rank": per_rank,
             "trials_max_over_mean": round(max(loads) / max(1e-9, float(np.mean(loads))), 4),
             "model_max_over_mean": round(max(costs) / max(1e-9, float(np.mean(costs))), 4),
@@ -325,6 +329,8 @@ def main():
                     help="2 = BASELINE config 2 (headline); paper; 5su (config-5 array, one user)")
     ap.add_argument("--check-launch", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-grid", action="store_true", help="skip the config-4 grid line (the 'grid' object)")
+    ap.add_argument("--grid-split", choices=["points", "trials"], default="points",
+                    help="the grid's multi-GPU split: whole points by cost (default), or every point's trials")
     ap.add_argument("--grid-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -446,7 +452,7 @@ def main():
         "ber": [round(float(x) / (total_trials * wl["S"] * np.log2(wl["M"])), 8) for x in err_tot],
     }
     if not args.no_grid and args.workload == "2" and args.precision == "f64":
-        out["grid"] = time_grid(rank, world, dist, dev, args.precision, tdev)
+        out["grid"] = time_grid(rank, world, dist, dev, args.precision, tdev, split=args.grid_split)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.workload, iters)
     if dist:

@@ -263,6 +263,18 @@ def wait_for_device_slot(dev: int, still_open, progress, stall_s: float = None, 
     return still_open()  # a slot freed because its holder finished the point: maybe done
 
 
+def _all_reduce_counts(dist, e, b, device=None):
+    """Sum one round's [points, counters] error / bit counts over the ranks (int64; on the
+    rank's GPU when the process group is RCCL's)."""
+    import torch
+    t = torch.from_numpy(np.stack([np.asarray(e, np.int64), np.asarray(b, np.int64)]))
+    if dist.get_backend() == "nccl":
+        t = t.to(torch.device("cuda", int(device) if device is not None else torch.cuda.current_device()))
+    dist.all_reduce(t)
+    t = t.cpu().numpy()
+    return t[0], t[1]
+
+
 class Link:
     """(mp_model.py:16-87)"""
 
@@ -440,7 +452,7 @@ class Link:
                     lock.release()
 
     def simulate_points(self, incl_clean_run: bool, reroll_chan: bool, cnc_n_iter_lst, seed_arrs, point_params,
-                        n_err, n_bits, stats: dict = None) -> None:
+                        n_err, n_bits, stats: dict = None, dist=None) -> None:
         """``simulate`` for many grid points of this system at once (the drivers' grid loops,
         main_mp_miso_cnc_constant_ber_req_ebn0_vs_ibo.py:100-215): every round launches one
         batch of every still-open point (mimo_engine_run_points); the counters of point i
@@ -448,8 +460,17 @@ class Link:
         rule and batch sizes as ``simulate`` would give them, so the totals are bit-identical.
         ``point_params[i]`` is ``point_params()`` captured at point i (after
         update_distortion / set_snr).  ``stats`` (a dict, optional) receives the work record:
-        ``trials`` per point, and per round the open points, trials and kernel ms."""
+        ``trials`` per point, and per round the open points, trials and kernel ms.
+
+        ``dist`` (torch.distributed with a process group, optional): the ranks share every
+        point's trials, as the reference's workers share one point's counters
+        (mp_model.py:177-187, the mp.Array).  Each round's batch of a point is split into
+        contiguous trial ranges, one per rank; the round's counts are summed over the ranks
+        (one all_reduce) before the stopping rule reads them, so every rank takes the same
+        decisions and the totals are bit-identical to one rank's (the few-points
+        alternative to dealing whole points).  Call it with the same points on every rank."""
         eng = self.engine(reroll_chan)
+        rank, world = (dist.get_rank(), dist.get_world_size()) if dist is not None else (0, 1)
         P = len(point_params)
         iters_all = np.asarray(cnc_n_iter_lst, dtype=np.int64).reshape(-1)
         uniq = sorted(set(int(i) for i in iters_all))
@@ -459,6 +480,7 @@ class Link:
             col = np.concatenate(([0], col))
         seeds = [_seed64(s) for s in seed_arrs]
         trial = np.zeros(P, dtype=np.int64)
+        ran = np.zeros(P, dtype=np.int64)  # trials this rank ran (= trial at world size 1)
         n_idx = len(col)
         for name, arr in (("n_err", n_err), ("n_bits", n_bits)):
             # added to in place: a copy (list, mp.Array, other dtype) would silently drop the totals
@@ -481,19 +503,37 @@ class Link:
             n = next_batch_rows(n_err[rows], n_bits[rows], act[rows], self.n_bits_per_ofdm_sym, self.n_err_min,
                                 self.bits_sent_max, self.max_batch)
             t0 = time.perf_counter()
-            e, b, _ = eng.run_points([mpoints[i] for i in rows], seeds_a[rows], trial[rows], n, uniq, incl_clean_run)
-            rounds.append(dict(points=int(rows.size), trials=int(n.sum()), kernel_ms=round(float(eng.kernel_ms), 3),
+            if world == 1:
+                e, b, _ = eng.run_points([mpoints[i] for i in rows], seeds_a[rows], trial[rows], n, uniq,
+                                         incl_clean_run)
+                ran[rows] += n
+                k_ms = float(eng.kernel_ms)
+            else:
+                n = np.asarray(n, dtype=np.int64)
+                lo, hi = n * rank // world, n * (rank + 1) // world  # this rank's trials of each point
+                ran[rows] += hi - lo
+                e = np.zeros((rows.size, len(uniq) + res_idx), np.int64)
+                b = np.zeros_like(e)
+                mine = np.flatnonzero(hi > lo)
+                k_ms = 0.0
+                if mine.size:
+                    em, bm, _ = eng.run_points([mpoints[i] for i in rows[mine]], seeds_a[rows[mine]],
+                                               trial[rows[mine]] + lo[mine], (hi - lo)[mine], uniq, incl_clean_run)
+                    e[mine], b[mine] = em.astype(np.int64), bm.astype(np.int64)
+                    k_ms = float(eng.kernel_ms)
+                e, b = _all_reduce_counts(dist, e, b, self.device)
+            rounds.append(dict(points=int(rows.size), trials=int(np.sum(n)), kernel_ms=round(k_ms, 3),
                                call_ms=round(1e3 * (time.perf_counter() - t0), 3)))
             if os.environ.get("MIMO_SWEEP_TRACE"):
                 import sys
                 print("simulate_points round: %d points, %d trials, kernel %.2f ms, call %.2f ms"
-                      % (rows.size, int(n.sum()), eng.kernel_ms, 1e3 * (time.perf_counter() - t0)), file=sys.stderr)
+                      % (rows.size, int(np.sum(n)), k_ms, 1e3 * (time.perf_counter() - t0)), file=sys.stderr)
             a = act[rows]
             n_err[rows] += np.where(a, e[:, col].astype(np.float64), 0.0)
             n_bits[rows] += np.where(a, b[:, col].astype(np.float64), 0.0)
             trial[rows] += n
         if stats is not None:
-            stats.update(trials=trial.copy(), rounds=rounds)
+            stats.update(trials=trial.copy(), trials_run=ran, rounds=rounds)
 
     def update_distortion(self, ibo_val_db: float) -> None:
         """(mp_model.py:230-241)"""

@@ -142,7 +142,7 @@ def point_costs(ibo_arr, ebn0_arr, n_bits_per_sym, constel_size, n_err_min, bits
 
 
 def run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean=True, seed=2137, rank=0, world=1, dist=None,
-             device=None, reroll_chan=True, multipoint=True, stats=None):
+             device=None, reroll_chan=True, multipoint=True, stats=None, split="points"):
     """Simulate every (IBO, Eb/N0) point this rank owns; all-reduce the counters.
 
     Returns (err, bits) int64 arrays of shape [n_ibo, n_ebn0, n_idx] on every rank.
@@ -153,7 +153,18 @@ def run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean=True, seed=2137, rank=0,
     stopping-rule rounds with their kernel ms, and the wall time of its share (before the
     all-reduce).  With a process group (``dist``), the counters are all-reduced even at
     world size 1 (one code path for every N).
+
+    ``split="trials"`` (with ``dist``; SURVEY §8(e)'s alternative for grids with few or very
+    unequal points, e.g. one BER-vs-Eb/N0 curve on 8 GPUs): every rank runs every point and
+    the ranks share each point's trials, one all-reduce of the round's counts per
+    stopping-rule round (``Link.simulate_points(dist=...)``).  The counts are bit-identical
+    to ``split="points"`` and to one rank.
     """
+    if split not in ("points", "trials"):
+        raise ValueError("split must be 'points' or 'trials'")
+    by_trials = split == "trials" and dist is not None
+    if by_trials and not (multipoint and hasattr(link, "simulate_points")):
+        raise ValueError("split='trials' needs a link with simulate_points (multipoint=True)")
     ibo_arr = np.asarray(ibo_arr, dtype=np.float64)
     ebn0_arr = np.asarray(ebn0_arr, dtype=np.float64)
     iters = np.asarray(iters)
@@ -166,7 +177,7 @@ def run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean=True, seed=2137, rank=0,
     costs = point_costs(ibo_arr, ebn0_arr, n_bits_sym, m.constel_size, getattr(link, "n_err_min", 1e5),
                         getattr(link, "bits_sent_max", 5e6), iters, getattr(link, "n_ant_val", 64),
                         getattr(link, "is_mcnc", False), chan)
-    mine = owned_points(n_pts, rank, world, costs)
+    mine = list(range(n_pts)) if by_trials else owned_points(n_pts, rank, world, costs)
     t_start = time.perf_counter()
     sim_stats = {}
     batched = multipoint and hasattr(link, "simulate_points")
@@ -192,23 +203,25 @@ def run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean=True, seed=2137, rank=0,
     if batched and mine:
         err = np.zeros((len(mine), n_idx))
         bits = np.zeros((len(mine), n_idx))
+        kw = dict(dist=dist) if by_trials else {}
         if stats is not None:
-            link.simulate_points(incl_clean, reroll_chan, iters, seeds, params, err, bits, stats=sim_stats)
-        else:
-            link.simulate_points(incl_clean, reroll_chan, iters, seeds, params, err, bits)
+            kw["stats"] = sim_stats
+        link.simulate_points(incl_clean, reroll_chan, iters, seeds, params, err, bits, **kw)
         counts[mine, :, 0] = err.astype(np.int64)
         counts[mine, :, 1] = bits.astype(np.int64)
     if stats is not None:
         # trials per point: all counters of a point share its trials; the longest-open one has
         # seen them all (bits / bits per symbol), also without simulate_points' record
-        trials = np.asarray(sim_stats.get("trials", counts[mine, :, 1].max(axis=1) // max(1, n_bits_sym)))
+        # (split by trials: the share of every point's trials this rank ran)
+        trials = np.asarray(sim_stats.get("trials_run", sim_stats.get("trials", counts[mine, :, 1].max(axis=1)
+                                                                      // max(1, n_bits_sym))))
         rounds = sim_stats.get("rounds", [])
         stats.update(rank=int(rank), points=len(mine), point_ids=[int(p) for p in mine],
                      cost_model=[float(costs[p]) for p in mine], trials_per_point=[int(x) for x in trials],
                      trials=int(np.sum(trials)), rounds=len(rounds),
                      kernel_ms=round(float(sum(r["kernel_ms"] for r in rounds)), 3), round_log=rounds,
                      wall_s=round(time.perf_counter() - t_start, 4))
-    if dist is not None:
+    if dist is not None and not by_trials:  # (by trials every rank already holds every total)
         import torch
         dev = torch.device(f"cuda:{device}") if device is not None and dist.get_backend() == "nccl" else None
         t = torch.from_numpy(counts).to(dev) if dev is not None else torch.from_numpy(counts)
@@ -310,6 +323,9 @@ def main():
     ap.add_argument("--n-err-min", type=int, default=int(1e5))
     ap.add_argument("--seed", type=int, default=2137)
     ap.add_argument("--out", type=str, default="figs/csv_results")
+    ap.add_argument("--split", choices=["points", "trials"], default="points",
+                    help="ranks deal whole points by cost (one all-reduce at the end), or share every point's "
+                         "trials (one all-reduce per stopping-rule round: for few / unequal points)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -327,7 +343,8 @@ def main():
     incl_clean = args.grid == "ber_vs_ebn0"
     link = _build_link(args, local)
     t0 = time.perf_counter()
-    err, bits = run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean, args.seed, rank, world, dist, local)
+    err, bits = run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean, args.seed, rank, world, dist, local,
+                         split=args.split)
     elapsed = time.perf_counter() - t0
     if rank == 0:
         ber = ber_from_counts(err, bits)

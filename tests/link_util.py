@@ -66,7 +66,7 @@ def simulate_child_counting(link, seed_arr, err, bits, created, iters=(0, 1)):
     link.simulate(True, True, np.asarray(iters), seed_arr, err, bits)
 
 
-def sweep_rank(rank, world, port, out, kw, ibo, ebn0, iters):
+def sweep_rank(rank, world, port, out, kw, ibo, ebn0, iters, split="points"):
     """One rank of a gloo-sharded sweep through the real Link -> engine path (all ranks on
     GPU 0, as MIMO_BENCH_BACKEND=gloo rehearses bench.py)."""
     import os
@@ -78,6 +78,6 @@ def sweep_rank(rank, world, port, out, kw, ibo, ebn0, iters):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     link, _ = build_link(device=0, **kw)
-    err, bits = sweep.run_grid(link, ibo, ebn0, iters, False, 11, rank, world, dist)
+    err, bits = sweep.run_grid(link, ibo, ebn0, iters, False, 11, rank, world, dist, split=split)
     np.save(os.path.join(out, "r%d.npy" % rank), np.stack([err, bits]))
     dist.destroy_process_group()

@@ -68,9 +68,11 @@ def test_multipoint_sweep_equals_sequential(receiver):
     assert np.all(bits <= 1024 * 300 + 64 * 1024)  # overshoot of at most one pilot batch
 
 
-def test_gloo_sharded_sweep_through_real_link_equals_single_process(tmp_path):
+@pytest.mark.parametrize("split", ["points", "trials"])
+def test_gloo_sharded_sweep_through_real_link_equals_single_process(tmp_path, split):
     """world_size 2 over gloo, both ranks on GPU 0, sweep.run_grid through the real
-    Link -> libmimo_engine path: equal to the single-process grid bit-for-bit."""
+    Link -> libmimo_engine path: equal to the single-process grid bit-for-bit, whether the
+    ranks deal the points or share every point's trials (one all_reduce per round)."""
     import os
     import socket
 
@@ -86,7 +88,7 @@ def test_gloo_sharded_sweep_through_real_link_equals_single_process(tmp_path):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    tmp.spawn(link_util.sweep_rank, args=(2, port, str(tmp_path), kw, ibo, ebn0, iters), nprocs=2, join=True)
+    tmp.spawn(link_util.sweep_rank, args=(2, port, str(tmp_path), kw, ibo, ebn0, iters, split), nprocs=2, join=True)
     for r in range(2):
         got = np.load(os.path.join(tmp_path, "r%d.npy" % r))
         np.testing.assert_array_equal(got[0], ref_err)
