@@ -510,7 +510,10 @@ class Link:
                 k_ms = float(eng.kernel_ms)
             else:
                 n = np.asarray(n, dtype=np.int64)
-                lo, hi = n * rank // world, n * (rank + 1) // world  # this rank's trials of each point
+                # this rank's trials of each point: share (rank + point) mod world of the batch, so
+                # the batches' remainders rotate over the ranks
+                sh = (rank + rows) % world
+                lo, hi = n * sh // world, n * (sh + 1) // world
                 ran[rows] += hi - lo
                 e = np.zeros((rows.size, len(uniq) + res_idx), np.int64)
                 b = np.zeros_like(e)
