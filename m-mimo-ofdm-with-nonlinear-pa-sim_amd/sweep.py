@@ -154,8 +154,8 @@ def run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean=True, seed=2137, rank=0,
     all-reduce).  With a process group (``dist``), the counters are all-reduced even at
     world size 1 (one code path for every N).
 
-    ``split="trials"`` (with ``dist``; SURVEY §8(e)'s alternative for grids with few or very
-    unequal points, e.g. one BER-vs-Eb/N0 curve on 8 GPUs): every rank runs every point and
+    ``split="trials"`` (with ``dist``; SURVEY §8(e)'s alternative for grids with fewer points
+    than ranks or a point count the ranks do not divide): every rank runs every point and
     the ranks share each point's trials, one all-reduce of the round's counts per
     stopping-rule round (``Link.simulate_points(dist=...)``).  The counts are bit-identical
     to ``split="points"`` and to one rank.
