@@ -160,8 +160,10 @@ def run_grid(link, ibo_arr, ebn0_arr, iters, incl_clean=True, seed=2137, rank=0,
     stopping-rule round (``Link.simulate_points(dist=...)``).  The counts are bit-identical
     to ``split="points"`` and to one rank.
     """
-    if split not in ("points", "trials"):
-        raise ValueError("split must be 'points' or 'trials'")
+    if split not in ("points", "trials", "auto"):
+        raise ValueError("split must be 'points', 'trials' or 'auto'")
+    if split == "auto":  # trials when some rank would get no point at all
+        split = "trials" if len(ibo_arr) * len(ebn0_arr) < world and hasattr(link, "simulate_points") else "points"
     by_trials = split == "trials" and dist is not None
     if by_trials and not (multipoint and hasattr(link, "simulate_points")):
         raise ValueError("split='trials' needs a link with simulate_points (multipoint=True)")
@@ -323,9 +325,10 @@ def main():
     ap.add_argument("--n-err-min", type=int, default=int(1e5))
     ap.add_argument("--seed", type=int, default=2137)
     ap.add_argument("--out", type=str, default="figs/csv_results")
-    ap.add_argument("--split", choices=["points", "trials"], default="points",
+    ap.add_argument("--split", choices=["points", "trials", "auto"], default="auto",
                     help="ranks deal whole points by cost (one all-reduce at the end), or share every point's "
-                         "trials (one all-reduce per stopping-rule round: for few / unequal points)")
+                         "trials (one all-reduce per stopping-rule round); auto: trials when there are fewer "
+                         "points than ranks")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

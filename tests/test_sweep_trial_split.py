@@ -111,3 +111,33 @@ def test_split_argument_checked():
     link, _ = _link()
     with pytest.raises(ValueError):
         sweep.run_grid(link, [0.0], [10.0], [0], split="bits")
+
+
+def _auto_worker(rank, world, port, out):
+    import torch.distributed as dist
+    import sweep
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    link, eng = _link()
+    st = {}
+    err, bits = sweep.run_grid(link, [1.0], [8.0], [0, 1], True, 3, rank, world, dist, split="auto", stats=st)
+    np.save(os.path.join(out, f"auto_r{rank}.npy"), np.stack([err, bits]))
+    np.save(os.path.join(out, f"auto_r{rank}_n.npy"), np.asarray([sum(eng.calls), st["points"]]))
+    dist.destroy_process_group()
+
+
+def test_auto_split_shares_a_single_point(tmp_path):
+    # one point, two ranks: "auto" shares its trials instead of leaving rank 1 idle
+    import sweep
+    link, eng = _link()
+    ref_err, ref_bits = sweep.run_grid(link, [1.0], [8.0], [0, 1], True, 3)
+    tmp.spawn(_auto_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    runs = []
+    for r in range(2):
+        got = np.load(os.path.join(tmp_path, f"auto_r{r}.npy"))
+        np.testing.assert_array_equal(got[0], ref_err)
+        np.testing.assert_array_equal(got[1], ref_bits)
+        n_tr, n_pts = np.load(os.path.join(tmp_path, f"auto_r{r}_n.npy"))
+        assert n_pts == 1
+        runs.append(n_tr)
+    assert sum(runs) == sum(eng.calls) and min(runs) > 0.4 * sum(runs)
