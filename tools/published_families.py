@@ -54,7 +54,13 @@ the reference saw no erroneous symbol in n_c trials.  With q the fraction of the
 trials that hold any bit error, that has probability (1 - q)^n_c; a point where that is
 below 1e-3 would be a mismatch.
 
+Where the published sigma rests on an assumed stopping rule, the reference's own re-runs
+calibrate it: tch() (three-cornered hat over published pairs, below) measures each run's scatter
+factor k and the engine's bias without that assumption; measure(k_ref=k) then scales the
+published variance (tests/test_gpu_published_pairs.py).
+
     python tools/published_families.py [--family csi|csi1|ebn0|ibo2|small2|toi|ibo|small|all] [--out file.json]
+    python tools/published_families.py --pairs [--out file.json]
 """
 from __future__ import annotations
 
