@@ -80,7 +80,11 @@ def reference_trials(pub_ber, bits_per_sym, per_counter=False):
     return np.minimum(budget, np.ceil(need.max(axis=-1)))
 
 
-def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137, n_ant=N_ANT, ibo_step=0.5):
+def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137, n_ant=N_ANT, ibo_step=0.5,
+        detail=None):
+    """The engine's grid against one published grid (module docstring).  ``detail`` (a dict,
+    optional) receives the per-cell arrays the comparison used: the replica sigma, the
+    reference's and the engine's trial counts per counter."""
     import sweep
     from utilities import ebn0_to_snr
     IBO = np.arange(0.0, 8.0, ibo_step)  # noqa: N806 (the grid of this published file)
@@ -121,6 +125,8 @@ def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137,
     # (same trial counts, same sigma model) -- a normal sample puts ~95 % within 2 sigma
     s_loo = est[:-1].std(axis=0, ddof=1)
     z_self = (est[-1] - est[:-1].mean(axis=0)) / np.maximum(s_loo * np.sqrt(1.0 + 1.0 / (reps - 1)), 1e-300)
+    if detail is not None:
+        detail.update(sig_rep=sig_rep, n_ref=n_ref, n_ref_c=n_ref_c, trials_c=trials_c, ibo=IBO)
     sel = pub >= 1e-3
     z = np.where(sel, (ber - pub) / sig, 0.0)
     rel = np.where(sel, np.abs(ber - pub) / np.maximum(pub, 1e-300), 0.0)
@@ -152,6 +158,35 @@ def run(channel="rayleigh", receiver="cnc", precision="f64", reps=16, seed=2137,
                                      max_abs_db=round(float(dreq.max()), 4) if dreq.size else None),
                spread=spread)
     return out, ber, pub, z
+
+
+def pair_check(channel, precision="f64", reps=16, seed=2137):
+    """Three-cornered hat (tools/published_families.py tch_solve) over the two published CNC
+    runs of one channel's grid: the 0.5-dB paper grid (run A) and the 0.25-dB grid (run B) at
+    the IBO values they share.  Per-trial spread from the replicas; each run's trials per counter
+    from its stopping rule; cells with published BER >= 1e-3 in both runs.  The IBO 0 row is
+    left out: it has the same grid index in both files, and over LoS the two runs agree there
+    to 0.12 % against ~1 % at every other IBO (the drivers' per-point seeds coincide)."""
+    import published_families as pf
+    det = {}
+    out, ber, pub_a, _ = run(channel, "cnc", precision, reps, seed, detail=det)
+    ibo_b, pub_b_all = published(channel, "cnc", N_ANT, 0.25)
+    ib = [int(np.flatnonzero(np.isclose(ibo_b, x))[0]) for x in det["ibo"]]
+    pub_b = pub_b_all[ib]
+    bits_per_sym = N_SC * int(np.log2(M))
+    n_a = det["n_ref_c"]
+    n_b = reference_trials(pub_b, bits_per_sym, per_counter=True)
+    sd = det["sig_rep"] * np.sqrt(det["n_ref"][..., None])      # per-trial spread
+    sel = (pub_a >= 1e-3) & (pub_b >= 1e-3) & (sd > 0)
+    sel[0] = False                                               # IBO 0: shared seeds
+    # [iteration, point] for tch_solve (the 9 counters of a point share its trials: resample points)
+    tr = lambda x: np.moveaxis(np.asarray(x, dtype=np.float64), -1, 0).reshape(len(ITERS), -1)  # noqa: E731
+    res = pf.tch_solve(tr(ber), tr(sd), tr(pub_a), tr(pub_b), tr(det["trials_c"]), tr(n_a), tr(n_b),
+                       np.moveaxis(sel, -1, 0).reshape(len(ITERS), -1))
+    res.update(channel=channel, precision=precision, grid_mean_z2=out["mean_z2"],
+               n_rule_a=float(np.median(n_a[sel])), n_rule_b=float(np.median(n_b[sel])))
+    res["bias_rms_2se"] = round(float(np.sqrt(max(0.0, res["beta"] + 2 * res["se_beta"]))), 4)
+    return res
 
 
 def spread_stats(z, sel, pub=None):
@@ -274,16 +309,24 @@ def run_baseline(channel="rayleigh", receiver="cnc", precision="f64", seed=2137)
     return out, ber
 
 
+def main_pairs(precision="f64"):
+    for ch in ("rayleigh", "los", "two_path"):
+        print(json.dumps(pair_check(ch, precision)), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--channel", default="rayleigh", choices=["rayleigh", "los", "two_path"])
     ap.add_argument("--receiver", default="cnc", choices=["cnc", "mcnc"])
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--out", default=None)
-    ap.add_argument("--grid", default="published", choices=["published", "baseline"])
+    ap.add_argument("--grid", default="published", choices=["published", "baseline", "pairs"])
     ap.add_argument("--n-ant", type=int, default=N_ANT)
     ap.add_argument("--ibo-step", type=float, default=0.5)
     a = ap.parse_args()
+    if a.grid == "pairs":  # three-cornered hat over the 0.5- and 0.25-dB published CNC grids
+        main_pairs(a.precision)
+        return
     if a.grid == "baseline":
         out, ber = run_baseline(a.channel, a.receiver, a.precision)
         print(json.dumps(out), flush=True)

@@ -418,16 +418,18 @@ def scatter_factors(res):
 
 def tch_solve(ber, sd, pa, pb, n_tr, n_a, n_b, sel, n_boot=1000, seed=0):
     """(k_a, k_b, beta) and their resampling standard errors from [row, point] arrays
-    (``sel``: the cells compared)."""
+    (``sel``: the cells compared; ``n_tr``: the engine's trials, a scalar or per cell)."""
     cols = np.flatnonzero(sel.any(axis=0))
     if cols.size < 4:
         return None
+
+    nt_all = np.broadcast_to(np.asarray(n_tr, dtype=np.float64), ber.shape)  # engine trials (scalar or per cell)
 
     def fit(idx):
         s = sel[:, idx]
         e, d, a, b = ber[:, idx][s], sd[:, idx][s], pa[:, idx][s], pb[:, idx][s]
         na, rho = n_a[:, idx][s], (n_a / n_b)[:, idx][s]
-        off = na / n_tr
+        off = na / nt_all[:, idx][s]
         U, V, W = na * ((e - a) / d) ** 2 - off, na * ((e - b) / d) ** 2 - off, na * ((a - b) / d) ** 2
         one, zero = np.ones_like(U), np.zeros_like(U)
         X = np.concatenate([np.stack([one, zero, one], 1), np.stack([zero, rho, one], 1), np.stack([one, rho, zero], 1)])
