@@ -27,8 +27,8 @@ CASES = [
     (2048, 1024, 8, 256, "softlim", 0.0, 0.0, None),  # 256-QAM at IBO 0 (strong clipping)
     (128, 4, 2, 16, "softlim", 0.0, -2.0, None),     # smallest band (4 sub-carriers), deep clipping
     # 2 antennas on 4-8 sub-carriers: the per-antenna precoding power strays far outside the
-    # alpha fit's |x| <= 0.25, so the fallback runs (alpha_fit.h segment table at F 2048 /
-    # 8192, the inline library form at F 4096)
+    # alpha fit's |x| <= 0.25, so the fallback runs (fp64: alpha_fit.h's segment table, out of
+    # line at every size since round 6; fp32: the library exp / erfc form)
     (2048, 8, 2, 16, "softlim", 0.0, 1.0, None),
     (4096, 8, 2, 16, "softlim", 0.0, 1.0, None),
     (8192, 4, 2, 16, "softlim", 0.0, 1.0, None),
