@@ -395,3 +395,44 @@ def test_cnc_mcnc_shared_rows_are_not_independent_runs():
         # independent runs of <= 1e7 bits: sigma_rel >= 1 / sqrt(BER 1e7) >= 1e-3 at BER <= 0.1
         sig = np.sqrt(2.0 / (a[r][m] * 1e7))
         assert np.median(rel / sig) < 0.2, np.median(rel / sig)
+
+
+def _nch_synthetic(ks, bias, seed, n_pts=40, n_rows=8, n_tr=8192):
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import published_families as pf
+    rng = np.random.default_rng(seed)
+    p = 10 ** rng.uniform(-4, -1.5, (n_rows, n_pts))
+    sd = 1.5 * np.sqrt(p / BPS)
+    n = np.minimum(814.0, np.ceil(1e5 / (p * BPS)))
+    e = p + bias * sd / np.sqrt(n) + rng.standard_normal(p.shape) * sd / np.sqrt(n_tr)
+    noise = [rng.standard_normal(p.shape) for _ in ks]
+    noise[1][:, :10] = noise[0][:, :10]          # runs 0 and 1 share their draws on points 0..9
+    pubs = [p + z * sd * np.sqrt(k / n) for z, k in zip(noise, ks)]
+    valid = [np.ones_like(p, bool) for _ in ks]
+    valid[2][:, 25:] = False                     # run 2 covers only part of the axis
+    same = [[np.zeros_like(p, bool) for _ in ks] for _ in ks]
+    same[0][1][:, :10] = same[1][0][:, :10] = True
+    return pf.nch_solve(e, sd, pubs, valid, n, n_tr, same, n_boot=300)
+
+
+@pytest.mark.parametrize("ks,bias", [((1.0, 1.0, 1.0), 0.0), ((2.5, 1.0, 4.0), 0.0), ((1.5, 1.5, 1.5), 1.0)])
+def test_nch_recovers_scatter_and_bias(ks, bias):
+    hits = 0
+    for seed in range(6):
+        r = _nch_synthetic(ks, bias, seed)
+        ok = all(abs(k - kt) <= 3 * s for k, kt, s in zip(r["k"], ks, r["se_k"]))
+        hits += ok and abs(r["beta"] - bias ** 2) <= 3 * r["se_beta"] + 0.05
+    assert hits >= 5
+
+
+def test_nch_hat_groups():
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import published_families as pf
+    gs = pf.hat_groups()
+    assert len(gs) == 6 and sum(len(g["runs"]) for g in gs) == 18
+    for g in gs:
+        c0 = g["runs"][0]
+        for c in g["runs"]:
+            assert (c["receiver"], c["channel"], c["ebn0"], c["bits_max"], c["n_err_min"]) == \
+                (c0["receiver"], c0["channel"], c0["ebn0"], c0["bits_max"], c0["n_err_min"])
+            assert pf.curve_name(c) not in pf.HAT_EXCLUDED

@@ -99,6 +99,8 @@ case $MODE in
     python -c "import json; [print(d['curve'], d['compared'], d['frac_abs_z_le1'], d['mean_z2'], d['max_abs_z'], d['median_abs_rel'], d['min_p_zero'], d['layout'], {k: v['mean_z2'] for k, v in d.items() if k.startswith('alt_')}) for d in json.load(open('$O/families_$fam.json'))]" ;;
   pairs)  # the three-cornered hat over the published re-run pairs + the calibrated csi1 curves
     timeout -k 10 900 python -u tools/published_families.py --pairs --out "$O/pairs.json" > "$O/pairs.log" 2> "$O/pairs.err" || exit $? ;;
+  hat)    # the N-cornered hat over the BER-vs-IBO re-run groups
+    timeout -k 10 900 python -u tools/published_families.py --hat --out "$O/hat.json" > "$O/hat.log" 2> "$O/hat.err" || exit $? ;;
   *)
     echo "unknown mode $MODE"; exit 2 ;;
 esac

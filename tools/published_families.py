@@ -444,6 +444,106 @@ def tch_solve(ber, sd, pa, pb, n_tr, n_a, n_b, sel, n_boot=1000, seed=0):
                 points=int(cols.size), cells=int(sel.sum()))
 
 
+# Files the published data alone flag as not runs of their stated configuration
+# (tests/test_published_data.py): not used as a corner.
+HAT_EXCLUDED = {"ibo2_cnc_los_nant64_ebn0_15_ibo0_8_0.5", "ibo_cnc_two_path_nant64_ebn0_15"}
+
+
+def hat_groups(min_runs=2):
+    """BER-vs-IBO files at 64 antennas that are independent runs of the same quantities: the
+    same receiver, channel and Eb/N0 (driver settings 1e7 bits / 1e5 errors for all), on IBO
+    grids that share points."""
+    import collections
+    g = collections.defaultdict(list)
+    for c in CURVES:
+        if c["family"] in ("ibo", "ibo2") and c["n_ant"] == 64 and curve_name(c) not in HAT_EXCLUDED:
+            g[(c["receiver"], c["channel"], c["ebn0"])].append(c)
+    return [dict(name="ibo_%s_%s_ebn0_%g" % k, runs=v) for k, v in sorted(g.items()) if len(v) >= min_runs]
+
+
+def nch_solve(ber, sd, pubs, valid, n_rule, n_tr, same_idx, n_boot=1000, seed=0):
+    """N-cornered hat: m published runs (``pubs[i]``, ``valid[i]``: [row, point]) of one rule
+    (``n_rule``: its trials per cell), the engine (``ber``, ``n_tr`` trials, per-trial spread
+    ``sd``).  In units of the rule's variance sd^2 / n_rule, per cell:
+      U_i  = n_rule ((e - p_i) / sd)^2 - n_rule / n_tr = k_i + beta
+      W_ij = n_rule ((p_i - p_j) / sd)^2               = k_i + k_j   (cells where ``same_idx[i][j]``
+                                                                      is False: independent draws)
+    Least squares for (k_1..k_m, beta); standard errors by resampling whole points."""
+    m = len(pubs)
+    P = ber.shape[1]
+    cols = np.flatnonzero(np.any([v.any(axis=0) for v in valid], axis=0))
+    nt_all = np.broadcast_to(np.asarray(n_tr, dtype=np.float64), ber.shape)
+
+    def fit(idx):
+        X, y = [], []
+        for i in range(m):
+            s = valid[i][:, idx]
+            n = n_rule[:, idx][s]
+            u = n * ((ber[:, idx][s] - pubs[i][:, idx][s]) / sd[:, idx][s]) ** 2 - n / nt_all[:, idx][s]
+            row = np.zeros(m + 1)
+            row[i], row[m] = 1.0, 1.0
+            X.append(np.tile(row, (u.size, 1)))
+            y.append(u)
+            for j in range(i + 1, m):
+                s2 = valid[i][:, idx] & valid[j][:, idx] & ~same_idx[i][j][:, idx]
+                n = n_rule[:, idx][s2]
+                w = n * ((pubs[i][:, idx][s2] - pubs[j][:, idx][s2]) / sd[:, idx][s2]) ** 2
+                row = np.zeros(m + 1)
+                row[i], row[j] = 1.0, 1.0
+                X.append(np.tile(row, (w.size, 1)))
+                y.append(w)
+        return np.linalg.lstsq(np.concatenate(X), np.concatenate(y), rcond=None)[0]
+
+    est = fit(cols)
+    rng = np.random.default_rng(seed)
+    boot = np.array([fit(rng.choice(cols, cols.size)) for _ in range(n_boot)])
+    se = boot.std(axis=0, ddof=1)
+    pairs = sum(int((valid[i] & valid[j] & ~same_idx[i][j]).sum()) for i in range(m) for j in range(i + 1, m))
+    return dict(k=[round(float(x), 4) for x in est[:m]], se_k=[round(float(x), 4) for x in se[:m]],
+                beta=round(float(est[m]), 4), se_beta=round(float(se[m]), 4), points=int(cols.size),
+                cells=int(sum(v.sum() for v in valid)), pair_cells=pairs)
+
+
+def nch(grp, n_tr=None, seed0=5150):
+    """The engine on the union of a hat group's IBO points; nch_solve over its runs (the counter
+    rows every run's layout holds)."""
+    runs = grp["runs"]
+    pubs_raw = [published(c) for c in runs]
+    axis = np.unique(np.round(np.concatenate([a for a, _ in pubs_raw]), 6))
+    c0 = runs[0]
+    if n_tr is None:
+        n_tr = 4096 if c0["receiver"] == "mcnc" else 8192
+    link, pts = points(c0, axis)
+    err, bits, per, dt = run_engine(link, pts, n_tr, seed0)
+    ber_all = (err / bits).T                                            # [engine column, point]
+    sd_all = (per.astype(np.float64) / BPS).std(axis=1, ddof=1).T
+    maps = [ROW_MAPS[layout(c, a, p)](p.shape[0]) for c, (a, p) in zip(runs, pubs_raw)]
+    common = sorted(set.intersection(*[set(mp) for mp in maps]))
+    ber, sd = ber_all[common], sd_all[common]
+    R, P = len(common), axis.size
+    pubs, valid, gidx = [], [], []
+    n_rule = stop_trials(ber, c0["bits_max"], c0["n_err_min"])
+    for c, (a, p), mp in zip(runs, pubs_raw, maps):
+        full = np.full((R, P), np.nan)
+        gi = np.full(P, -1)
+        for j, x in enumerate(axis):
+            hit = np.flatnonzero(np.isclose(a, x))
+            if hit.size:
+                full[:, j] = p[[mp.index(col) for col in common], hit[0]]
+                gi[j] = hit[0]
+        ok = np.isfinite(full) & (full >= 1e-5) & (np.nan_to_num(full) * n_rule * BPS >= 100) & (sd > 0)
+        pubs.append(np.nan_to_num(full))
+        valid.append(ok)
+        gidx.append(gi)
+    m = len(runs)
+    same = [[np.broadcast_to((gidx[i] == gidx[j]) & (gidx[i] >= 0), (R, P)) for j in range(m)] for i in range(m)]
+    res = nch_solve(ber, sd, pubs, valid, n_rule, n_tr, same)
+    res.update(group=grp["name"], runs=[curve_name(c) for c in runs], rows=R, n_tr=n_tr, seconds=round(dt, 2),
+               n_rule_median=float(np.median(n_rule[np.any(valid, axis=0)])) if any(v.any() for v in valid) else None)
+    res["bias_rms_2se"] = round(float(np.sqrt(max(0.0, res["beta"] + 2 * res["se_beta"]))), 4)
+    return res
+
+
 def tch(p, n_tr=None, seed0=5150):
     """The engine at the common points of a published pair; tch_solve's figures, plus each run's
     effective trial count (its rule's median over k)."""
@@ -484,7 +584,18 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--n-tr", type=int, default=None)
     ap.add_argument("--pairs", action="store_true", help="the three-cornered hat over the published re-run pairs")
+    ap.add_argument("--hat", action="store_true", help="the N-cornered hat over the BER-vs-IBO re-run groups")
     a = ap.parse_args()
+    if a.hat:
+        res = []
+        for g in hat_groups():
+            r = nch(g, a.n_tr)
+            print(json.dumps(r), flush=True)
+            res.append(r)
+        if a.out:
+            with open(a.out, "w") as f:
+                json.dump(res, f, indent=1)
+        return
     if a.pairs:
         res = []
         for p in pairs():
