@@ -207,6 +207,27 @@ def load_pmc_traffic(workload, iters, precision, trials_per_launch):
     return None, None
 
 
+def ber_vs_published(ber):
+    """BASELINE's "BER match vs ref" for the config-2 line: the reference's published standard-RX
+    BER at the same point (tests/golden/published_ber_vs_ebn0_cnc_rayleigh_ibo3.csv, a data file
+    of its figs/csv_results: 64 antennas, Rayleigh, MRT, soft limiter IBO 3 dB, 64-QAM, Eb/N0
+    15 dB; rows [no distortion, standard RX, CNC 1..8]).  Its geometry is 2048 sub-carriers /
+    FFT 4096, config 2's 1024 / 2048: the same F = 2S, so the same per-sub-carrier statistics.
+    z against the published run's binomial sigma (its 1e7-bit budget,
+    main_mp_miso_cnc_ber_vs_ebn0.py: bits within a symbol treated as independent, so |z| is an
+    upper bound); tests/test_gpu_link.py holds the full-curve comparison."""
+    path = os.path.join(REPO, "tests", "golden", "published_ber_vs_ebn0_cnc_rayleigh_ibo3.csv")
+    try:
+        rows = np.loadtxt(path, delimiter=",")
+    except OSError:
+        return None
+    pub = float(rows[2][int(np.flatnonzero(np.isclose(rows[0], 15.0))[0])])
+    sig = pub / np.sqrt(pub * 1e7)
+    return {"engine": ber, "published": pub, "rel": round(ber / pub - 1, 5), "z_binomial": round(float((ber - pub) / sig), 3),
+            "source": "tests/golden/published_ber_vs_ebn0_cnc_rayleigh_ibo3.csv (standard RX, Eb/N0 15 dB; "
+                      "2048-sc / FFT-4096 geometry, F = 2S as config 2)"}
+
+
 def launch_ranks(n):
     """``--gpus N`` without an outer torchrun: start ``torch.distributed.run`` with N ranks
     as a CHILD process (this parent has made no GPU call and never execs), forward rank 0's
@@ -451,6 +472,8 @@ def main():
                         "trials; the fused kernel does not move them (a model figure, not traffic)"},
         "ber": [round(float(x) / (total_trials * wl["S"] * np.log2(wl["M"])), 8) for x in err_tot],
     }
+    if args.workload == "2" and iters == [0]:
+        out["ber_vs_published"] = ber_vs_published(out["ber"][0])
     if not args.no_grid and args.workload == "2" and args.precision == "f64":
         out["grid"] = time_grid(rank, world, dist, dev, args.precision, tdev, split=args.grid_split)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
