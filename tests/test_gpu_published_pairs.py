@@ -45,7 +45,7 @@ def pair_results():
 def test_published_pair_engine_unbiased(pair_results, i):
     r = pair_results[i]
     print({k: v for k, v in r.items() if k not in ("a", "b")})
-    assert r["points"] >= 16 and r["cells"] >= 140
+    assert r["points"] >= 15 and r["cells"] >= 120  # (Eb/N0 5 dB, index 0 in both grids, not used)
     # each published run's scatter against its rule is a real, finite variance
     assert 0.1 <= r["k_a"] <= 8 and 0.1 <= r["k_b"] <= 8
     assert r["beta"] - 2 * r["se_beta"] <= 0.0, r
