@@ -318,7 +318,8 @@ def main():
     ap.add_argument("--channel", choices=["rayleigh", "los", "two_path"], default="rayleigh")
     ap.add_argument("--receiver", choices=["cnc", "mcnc"], default="cnc")
     ap.add_argument("--ibo", type=str, default="0:8:0.5", help="start:stop:step (numpy arange)")
-    ap.add_argument("--ebn0", type=str, default="10:23.1:0.5")
+    ap.add_argument("--ebn0", type=str, default="10:22.1:0.5",
+                    help="start:stop:step (numpy arange); default: the published fixed-BER grids' Eb/N0 10..22 dB")
     ap.add_argument("--iters", type=str, default="0,1,2,3,4,5,6,7,8")
     ap.add_argument("--target-ber", type=float, default=1e-2)
     ap.add_argument("--bits-sent-max", type=int, default=int(5e6))
