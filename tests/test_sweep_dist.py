@@ -83,3 +83,22 @@ def test_sweep_shards_cover_and_balance():
         assert sorted(p for q in parts for p in q) == list(range(len(costs)))
         loads = [costs[q].sum() for q in parts]
         assert max(loads) <= min(loads) + costs.max()
+
+
+def test_cli_default_grid_is_the_published_one():
+    # sweep.py's default --ibo / --ebn0 axes give the published fixed-BER grids' points
+    # (header: the IBO axis; one row of 9 counters per (IBO, Eb/N0) point)
+    import argparse
+    import sweep
+    src = open(sweep.__file__).read()
+    ibo = [a for a in src.split("\n") if '"--ibo"' in a][0].split('default="')[1].split('"')[0]
+    ebn0 = [a for a in src.split("\n") if '"--ebn0"' in a][0].split('default="')[1].split('"')[0]
+    rng = lambda s: np.arange(*[float(x) for x in s.split(":")])  # noqa: E731
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    f = ("published_fixed_ber1.0e-02_cnc_rayleigh_nant64_ebn0_min10_max22_step0.50_ibo_min0_max7_step0.50_"
+         "niter1_2_3_4_5_6_7_8.csv")
+    lines = open(os.path.join(d, f)).read().strip().split("\n")
+    np.testing.assert_allclose(rng(ibo), np.array(lines[0].split(","), dtype=float))
+    assert len(rng(ibo)) * len(rng(ebn0)) == len(lines) - 1
+    assert rng(ebn0)[0] == 10.0 and rng(ebn0)[-1] == 22.0
+    del argparse
