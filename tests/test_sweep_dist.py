@@ -88,7 +88,6 @@ def test_sweep_shards_cover_and_balance():
 def test_cli_default_grid_is_the_published_one():
     # sweep.py's default --ibo / --ebn0 axes give the published fixed-BER grids' points
     # (header: the IBO axis; one row of 9 counters per (IBO, Eb/N0) point)
-    import argparse
     import sweep
     src = open(sweep.__file__).read()
     ibo = [a for a in src.split("\n") if '"--ibo"' in a][0].split('default="')[1].split('"')[0]
@@ -101,4 +100,3 @@ def test_cli_default_grid_is_the_published_one():
     np.testing.assert_allclose(rng(ibo), np.array(lines[0].split(","), dtype=float))
     assert len(rng(ibo)) * len(rng(ebn0)) == len(lines) - 1
     assert rng(ebn0)[0] == 10.0 and rng(ebn0)[-1] == 22.0
-    del argparse
